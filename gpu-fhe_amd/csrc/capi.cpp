@@ -1,0 +1,237 @@
+// extern "C" entry points of libfhecore (declared in include/fhecore.h): argument checking,
+// error reporting and workspace handling around the HIP launchers.
+#include "../../include/fhecore.h"
+
+#include <string>
+
+#include "internal.hpp"
+
+namespace fhe {
+
+namespace {
+thread_local std::string g_last_error;
+
+inline hipStream_t hs(fhe_stream_t s) { return static_cast<hipStream_t>(s); }
+
+int check_window(const fhe_ctx* c, uint32_t limb0, uint32_t nlimbs, uint32_t limit,
+                 const char* who) {
+  if (!c) {
+    set_error(std::string(who) + ": null context");
+    return kInvalid;
+  }
+  if ((uint64_t)limb0 + nlimbs > limit) {
+    set_error(std::string(who) + ": limb window [" + std::to_string(limb0) + ", " +
+              std::to_string(limb0 + nlimbs) + ") exceeds " + std::to_string(limit) + " limbs");
+    return kInvalid;
+  }
+  return kOk;
+}
+
+// Internal workspace (grows on demand; allocation makes this path non-capturable).
+int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws) {
+  if (*ws) return kOk;
+  auto* c = const_cast<fhe_ctx*>(cc);
+  if (c->workspace_bytes < bytes) {
+    if (c->workspace) FHE_HIP_CHECK(hipFree(c->workspace));
+    c->workspace = nullptr;
+    c->workspace_bytes = 0;
+    FHE_HIP_CHECK(hipMalloc(&c->workspace, bytes));
+    c->workspace_bytes = bytes;
+  }
+  *ws = c->workspace;
+  return kOk;
+}
+
+}  // namespace
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+}  // namespace fhe
+
+using namespace fhe;
+
+extern "C" {
+
+const char* fhe_last_error(void) { return g_last_error.c_str(); }
+
+const char* fhe_version(void) { return "fhecore 0.1 (gfx950)"; }
+
+int fhe_gen_moduli(uint32_t log_n, uint32_t count, uint32_t bits, uint32_t skip, uint64_t* out) {
+  if (!out && count) {
+    set_error("fhe_gen_moduli: null output");
+    return kInvalid;
+  }
+  return gen_moduli(log_n, count, bits, skip, out);
+}
+
+int fhe_ctx_create(fhe_ctx** ctx, uint32_t log_n, const uint64_t* q, uint32_t L,
+                   const uint64_t* p, uint32_t K, uint32_t dnum, int device) {
+  if (!q || (K && !p)) {
+    set_error("fhe_ctx_create: null modulus array");
+    return kInvalid;
+  }
+  try {
+    return ctx_create(ctx, log_n, q, L, p, K, dnum, device);
+  } catch (const std::exception& e) {
+    set_error(std::string("fhe_ctx_create: ") + e.what());
+    return kNoMem;
+  }
+}
+
+int fhe_ctx_destroy(fhe_ctx* ctx) { return ctx_destroy(ctx); }
+
+int fhe_ctx_moduli(const fhe_ctx* c, uint64_t* moduli, uint64_t* psi) {
+  if (!c) {
+    set_error("fhe_ctx_moduli: null context");
+    return kInvalid;
+  }
+  for (size_t i = 0; i < c->moduli.size(); ++i) {
+    if (moduli) moduli[i] = c->moduli[i];
+    if (psi) psi[i] = c->psi[i];
+  }
+  return kOk;
+}
+
+int fhe_ctx_shape(const fhe_ctx* c, uint32_t* log_n, uint32_t* L, uint32_t* K, uint32_t* dnum,
+                  int* device) {
+  if (!c) {
+    set_error("fhe_ctx_shape: null context");
+    return kInvalid;
+  }
+  if (log_n) *log_n = c->log_n;
+  if (L) *L = c->L;
+  if (K) *K = c->K;
+  if (dnum) *dnum = c->dnum;
+  if (device) *device = c->device;
+  return kOk;
+}
+
+int fhe_ctx_reserve(fhe_ctx* c, size_t bytes) {
+  if (!c) {
+    set_error("fhe_ctx_reserve: null context");
+    return kInvalid;
+  }
+  void* ws = nullptr;
+  return ensure_ws(c, bytes, &ws);
+}
+
+static int vec_ctx(int op, const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                   uint32_t polys, uint32_t limb0, uint32_t nlimbs, fhe_stream_t s,
+                   const char* who) {
+  int rc = check_window(c, limb0, nlimbs, c ? c->L + c->K : 0, who);
+  if (rc) return rc;
+  if ((!out || !a || !b) && (uint64_t)polys * nlimbs) {
+    set_error(std::string(who) + ": null data pointer");
+    return kInvalid;
+  }
+  return launch_vec_ctx(c, op, out, a, b, polys, limb0, nlimbs, hs(s));
+}
+
+int fhe_vec_add(const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                uint32_t polys, uint32_t limb0, uint32_t nlimbs, fhe_stream_t s) {
+  return vec_ctx(kAdd, c, out, a, b, polys, limb0, nlimbs, s, "fhe_vec_add");
+}
+int fhe_vec_sub(const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                uint32_t polys, uint32_t limb0, uint32_t nlimbs, fhe_stream_t s) {
+  return vec_ctx(kSub, c, out, a, b, polys, limb0, nlimbs, s, "fhe_vec_sub");
+}
+int fhe_vec_mul(const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                uint32_t polys, uint32_t limb0, uint32_t nlimbs, fhe_stream_t s) {
+  return vec_ctx(kMul, c, out, a, b, polys, limb0, nlimbs, s, "fhe_vec_mul");
+}
+
+int fhe_vec_op_mod(int op, uint64_t* out, const uint64_t* a, const uint64_t* b, uint64_t rows,
+                   uint64_t cols, const uint64_t* mods, uint64_t mod_stride, int signed_in,
+                   int device, fhe_stream_t s) {
+  if (op < kAdd || op > kMul) {
+    set_error("fhe_vec_op_mod: op must be 0 (add), 1 (sub) or 2 (mul)");
+    return kInvalid;
+  }
+  if (rows * cols == 0) return kOk;
+  if (!out || !a || !b || !mods) {
+    set_error("fhe_vec_op_mod: null pointer");
+    return kInvalid;
+  }
+  const uint64_t nm = mod_stride ? (rows - 1) * mod_stride + 1 : 1;
+  std::vector<ModParams> mp(nm);
+  for (uint64_t i = 0; i < nm; ++i) {
+    if (mods[i] < 2) {
+      set_error("fhe_vec_op_mod: modulus must be >= 2");
+      return kInvalid;
+    }
+    mp[i] = make_mod_params(mods[i]);
+  }
+  FHE_HIP_CHECK(hipSetDevice(device));
+  ModParams* d = nullptr;
+  FHE_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d), nm * sizeof(ModParams), hs(s)));
+  FHE_HIP_CHECK(hipMemcpyAsync(d, mp.data(), nm * sizeof(ModParams), hipMemcpyHostToDevice, hs(s)));
+  const int rc = launch_vec_mod(op, out, a, b, rows, cols, d, mod_stride, signed_in, hs(s));
+  FHE_HIP_CHECK(hipStreamSynchronize(hs(s)));  // mp must outlive the async copy
+  FHE_HIP_CHECK(hipFreeAsync(d, hs(s)));
+  return rc;
+}
+
+int fhe_ntt_fwd(const fhe_ctx* c, uint64_t* data, uint32_t polys, uint32_t limb0,
+                uint32_t nlimbs, fhe_stream_t s) {
+  int rc = check_window(c, limb0, nlimbs, c ? c->L + c->K : 0, "fhe_ntt_fwd");
+  if (rc) return rc;
+  return launch_ntt(c, true, data, data, polys, (uint64_t)nlimbs * c->n, limb0, nlimbs, hs(s));
+}
+
+int fhe_ntt_inv(const fhe_ctx* c, uint64_t* data, uint32_t polys, uint32_t limb0,
+                uint32_t nlimbs, fhe_stream_t s) {
+  int rc = check_window(c, limb0, nlimbs, c ? c->L + c->K : 0, "fhe_ntt_inv");
+  if (rc) return rc;
+  return launch_ntt(c, false, data, data, polys, (uint64_t)nlimbs * c->n, limb0, nlimbs, hs(s));
+}
+
+size_t fhe_hommult_workspace(const fhe_ctx* c, uint32_t batch, uint32_t nlimbs) {
+  return c ? hommult_workspace_bytes(c, batch, nlimbs) : 0;
+}
+
+int fhe_hommult(const fhe_ctx* c, uint64_t* d, const uint64_t* a, const uint64_t* b,
+                uint32_t batch, uint32_t limb0, uint32_t nlimbs, void* ws, fhe_stream_t s) {
+  int rc = check_window(c, limb0, nlimbs, c ? c->L : 0, "fhe_hommult");
+  if (rc) return rc;
+  if ((rc = ensure_ws(c, hommult_workspace_bytes(c, batch, nlimbs), &ws))) return rc;
+  return launch_hommult(c, d, a, b, batch, limb0, nlimbs, ws, hs(s));
+}
+
+int fhe_baseconv(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t s0, uint32_t S,
+                 uint32_t t0, uint32_t T, fhe_stream_t s) {
+  if (!c) {
+    set_error("fhe_baseconv: null context");
+    return kInvalid;
+  }
+  return launch_baseconv(c, out, in, s0, S, t0, T, hs(s));
+}
+
+size_t fhe_keyswitch_workspace(const fhe_ctx* c, uint32_t nlimbs) {
+  return c ? keyswitch_workspace_bytes(c, nlimbs) : 0;
+}
+
+int fhe_keyswitch_shard(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t* c_all,
+                        const uint64_t* d2_own, const uint64_t* evk_b, const uint64_t* evk_a,
+                        uint32_t limb0, uint32_t nlimbs, void* ws, fhe_stream_t s) {
+  int rc = check_window(c, limb0, nlimbs, c ? c->L : 0, "fhe_keyswitch_shard");
+  if (rc) return rc;
+  if ((rc = ensure_ws(c, keyswitch_workspace_bytes(c, nlimbs), &ws))) return rc;
+  return launch_keyswitch_shard(c, ks0, ks1, c_all, d2_own, evk_b, evk_a, limb0, nlimbs, ws,
+                                hs(s));
+}
+
+int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t* d2,
+                  const uint64_t* evk_b, const uint64_t* evk_a, void* ws, fhe_stream_t s) {
+  int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_keyswitch");
+  if (rc) return rc;
+  if ((rc = ensure_ws(c, keyswitch_workspace_bytes(c, c->L), &ws))) return rc;
+  // c_all = INTT(d2) lives at the tail of the workspace
+  const size_t tail = keyswitch_workspace_bytes(c, c->L) - (size_t)c->L * c->n * sizeof(uint64_t);
+  uint64_t* c_all = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + tail);
+  FHE_HIP_CHECK(hipMemcpyAsync(c_all, d2, (size_t)c->L * c->n * sizeof(uint64_t),
+                               hipMemcpyDeviceToDevice, hs(s)));
+  if ((rc = launch_ntt(c, false, c_all, c_all, 1, 0, 0, c->L, hs(s)))) return rc;
+  return launch_keyswitch_shard(c, ks0, ks1, c_all, d2, evk_b, evk_a, 0, c->L, ws, hs(s));
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+// Coefficient-wise modular add / sub / mul: the reference's vec_add / vec_sub / vec_mul
+// (/root/reference/arithmetic.py:3-13; vec_mul in the NTT domain = poly_mul_pointwise).
+//
+// Two entry families:
+//  * context kernels: canonical residues in [0, q_l) for the context's limb moduli, layout
+//    [polys][nlimbs][N]; one 16-byte load per operand per lane (HBM-bound, 24 B/elem);
+//  * generic kernels for the reference-shaped Python API: any u64 (or signed i64) inputs, any
+//    modulus 2 <= q < 2^64, one modulus per row (scalar MOD or a (L, 1) MOD column); results
+//    equal Python's exact `(a op b) % MOD` (the object-dtype semantics).
+#include "internal.hpp"
+
+namespace fhe {
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ u64 op_canon(int op, u64 a, u64 b, const ModParams& m) {
+  if (op == kAdd) return csub(a + b, m.q);
+  if (op == kSub) return a >= b ? a - b : a + (m.q - b);
+  return mulmod_barrett(a, b, m);
+}
+
+template <int OP>
+__global__ __launch_bounds__(kThreads) void k_vec_ctx(u64* __restrict__ out,
+                                                      const u64* __restrict__ a,
+                                                      const u64* __restrict__ b, u64 pairs,
+                                                      u32 log_n, u32 nlimbs, u32 limb0,
+                                                      const ModParams* __restrict__ mods) {
+  // each lane handles 2 adjacent coefficients (16-byte accesses); N >= 2 so a pair never
+  // straddles limbs.
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < pairs; i += stride) {
+    const u64 e = 2 * i;
+    const u32 limb = limb0 + (u32)((e >> log_n) % nlimbs);
+    const ModParams m = mods[limb];
+    const ulonglong2 x = reinterpret_cast<const ulonglong2*>(a)[i];
+    const ulonglong2 y = reinterpret_cast<const ulonglong2*>(b)[i];
+    ulonglong2 r;
+    r.x = op_canon(OP, x.x, y.x, m);
+    r.y = op_canon(OP, x.y, y.y, m);
+    reinterpret_cast<ulonglong2*>(out)[i] = r;
+  }
+}
+
+__device__ __forceinline__ u64 to_residue(u64 x, int signed_in, const ModParams& m) {
+  if (signed_in && (int64_t)x < 0) {
+    // x = -(|x|): |x| mod q, negated
+    const u64 r = reduce_u64((u64)0 - x, m);
+    return r == 0 ? 0 : m.q - r;
+  }
+  return reduce_u64(x, m);
+}
+
+template <int OP>
+__global__ __launch_bounds__(kThreads) void k_vec_mod(u64* __restrict__ out,
+                                                      const u64* __restrict__ a,
+                                                      const u64* __restrict__ b, u64 rows,
+                                                      u64 cols, const ModParams* __restrict__ mods,
+                                                      u64 mod_stride, int signed_in) {
+  const u64 total = rows * cols;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const ModParams m = mods[(i / cols) * mod_stride];
+    const u64 x = to_residue(a[i], signed_in, m), y = to_residue(b[i], signed_in, m);
+    u64 r;
+    if (OP == kAdd) r = x >= m.q - y ? x - (m.q - y) : x + y;
+    else if (OP == kSub) r = x >= y ? x - y : x + (m.q - y);
+    else r = mulmod_any(x, y, m);
+    out[i] = r;
+  }
+}
+
+inline u32 grid_for(u64 work) {
+  const u64 blocks = (work + kThreads - 1) / kThreads;
+  return (u32)(blocks < 256 * 16 ? (blocks ? blocks : 1) : 256 * 16);
+}
+
+}  // namespace
+
+int launch_vec_ctx(const fhe_ctx* c, int op, u64* out, const u64* a, const u64* b, u32 polys,
+                   u32 limb0, u32 nlimbs, hipStream_t s) {
+  const u64 pairs = (u64)polys * nlimbs * c->n / 2;
+  if (pairs == 0) return kOk;
+  const u32 g = grid_for(pairs);
+  switch (op) {
+    case kAdd: k_vec_ctx<kAdd><<<g, kThreads, 0, s>>>(out, a, b, pairs, c->log_n, nlimbs, limb0, c->d_mods); break;
+    case kSub: k_vec_ctx<kSub><<<g, kThreads, 0, s>>>(out, a, b, pairs, c->log_n, nlimbs, limb0, c->d_mods); break;
+    case kMul: k_vec_ctx<kMul><<<g, kThreads, 0, s>>>(out, a, b, pairs, c->log_n, nlimbs, limb0, c->d_mods); break;
+    default: set_error("bad vec op"); return kInvalid;
+  }
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+
+int launch_vec_mod(int op, u64* out, const u64* a, const u64* b, u64 rows, u64 cols,
+                   const ModParams* d_mods, u64 mod_stride, int signed_in, hipStream_t s) {
+  const u64 total = rows * cols;
+  if (total == 0) return kOk;
+  const u32 g = grid_for(total);
+  switch (op) {
+    case kAdd: k_vec_mod<kAdd><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, mod_stride, signed_in); break;
+    case kSub: k_vec_mod<kSub><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, mod_stride, signed_in); break;
+    case kMul: k_vec_mod<kMul><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, mod_stride, signed_in); break;
+    default: set_error("bad vec op"); return kInvalid;
+  }
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+
+}  // namespace fhe

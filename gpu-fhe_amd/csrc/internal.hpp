@@ -1,0 +1,107 @@
+// Library-internal context and launcher declarations for libfhecore (not installed).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "modarith.hpp"
+
+namespace fhe {
+
+// Status codes shared with include/fhecore.h.
+enum Status : int {
+  kOk = 0,
+  kInvalid = -1,
+  kNoMem = -2,
+  kDevice = -3,
+  kUnsupported = -4,
+};
+
+void set_error(const std::string& msg);
+
+
+}  // namespace fhe
+
+// Immutable after fhe_ctx_create, except for the lazily grown internal workspace.
+struct fhe_ctx {
+  int device = 0;
+  uint32_t log_n = 0;
+  uint64_t n = 0;
+  uint32_t L = 0, K = 0, dnum = 0, alpha = 0;
+  std::vector<uint64_t> moduli;  // L Q-primes then K P-primes
+  std::vector<uint64_t> psi;     // primitive 2N-th roots, per modulus
+  std::vector<fhe::ModParams> mods_host;
+
+  fhe::ModParams* d_mods = nullptr;  // [L + K]
+  ulonglong2* d_tw_fwd = nullptr;    // [L + K][N] (psi^brv(k), Shoup)
+  ulonglong2* d_tw_inv = nullptr;    // [L + K][N] (psi^-brv(k), Shoup)
+  ulonglong2* d_nfold = nullptr;     // [L + K][2] (N^-1, psi^-1 N^-1) with Shoup
+
+  // Hybrid key-switch base-conversion constants (rns.hip), Shoup pairs, device resident.
+  // Digit j covers Q-limbs [j * alpha, min(L, (j + 1) * alpha)).
+  ulonglong2* d_modup_inv = nullptr;    // [dnum][alpha]        (D^_k)^-1 mod q_k
+  ulonglong2* d_modup_hat = nullptr;    // [dnum][alpha][L + K] D^_k mod t  (by ctx limb t)
+  ulonglong2* d_moddown_inv = nullptr;  // [K]                  (P^_k)^-1 mod p_k
+  ulonglong2* d_moddown_hat = nullptr;  // [K][L + K]           P^_k mod q_i
+  ulonglong2* d_pinv = nullptr;         // [L]                  P^-1 mod q_i
+
+  void* workspace = nullptr;
+  size_t workspace_bytes = 0;
+};
+
+namespace fhe {
+
+// ---- launchers (ntt.hip) ---------------------------------------------------------------
+// data layout [polys][nlimbs][N] with poly stride `pstride` (elements); limb l uses table limb0 + l.
+int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 polys, u64 pstride,
+               u32 limb0, u32 nlimbs, hipStream_t s);
+// Fused ct x ct tensor: a, b [batch][2][nlimbs][N] coefficient form -> d [batch][3][nlimbs][N].
+int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
+                   u32 nlimbs, void* ws, hipStream_t s);
+size_t hommult_workspace_bytes(const fhe_ctx* c, u32 batch, u32 nlimbs);
+
+// ---- launchers (elementwise.hip) -------------------------------------------------------
+enum VecOp : int { kAdd = 0, kSub = 1, kMul = 2 };
+int launch_vec_ctx(const fhe_ctx* c, int op, u64* out, const u64* a, const u64* b, u32 polys,
+                   u32 limb0, u32 nlimbs, hipStream_t s);
+int launch_vec_mod(int op, u64* out, const u64* a, const u64* b, u64 rows, u64 cols,
+                   const ModParams* d_mods, u64 mod_stride, int signed_in, hipStream_t s);
+
+// ---- launchers (rns.hip) --------------------------------------------------------------
+// Per-rank body of the hybrid key-switch (SURVEY.md §8a', §8e): c_all [L][N] coefficient form of
+// the whole d2 (all-gathered), d2_own [nlimbs][N] NTT form of this rank's Q-limbs
+// [limb0, limb0 + nlimbs), evk_b/evk_a [dnum][nlimbs + K][N] NTT form (own Q-limbs then P).
+// ks0/ks1 [nlimbs][N] NTT form.
+int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_all,
+                           const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
+                           u32 nlimbs, void* ws, hipStream_t s);
+size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs);
+// Fast basis extension between contiguous ctx limb ranges: in [S][N] over limbs [s0, s0+S),
+// out [T][N] over limbs [t0, t0+T) (ranges disjoint).
+int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u32 t0, u32 T,
+                    hipStream_t s);
+
+// ---- host (context.cpp) ----------------------------------------------------------------
+int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 K, u32 dnum,
+               int device);
+int ctx_destroy(fhe_ctx* c);
+int gen_moduli(u32 log_n, u32 count, u32 bits, u32 skip, u64* out);
+int build_rns_tables(fhe_ctx* c);
+ModParams make_mod_params(u64 q);
+bool is_prime_u64(u64 n);
+u64 powmod_u64(u64 b, u64 e, u64 q);
+u64 mulmod_u64(u64 a, u64 b, u64 q);
+u64 find_psi(u64 q, u32 log_n);
+
+}  // namespace fhe
+
+#define FHE_HIP_CHECK(expr)                                                             \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      fhe::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                \
+      return fhe::kDevice;                                                              \
+    }                                                                                   \
+  } while (0)

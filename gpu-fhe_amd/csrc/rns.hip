@@ -1,0 +1,303 @@
+// RNS fast base conversion, ModUp / ModDown and the hybrid key-switch inner product (gfx950).
+//
+// None of this exists in the reference; the spec is SURVEY.md §8a':
+//   baseconv   y_k = [x_k (S^_k)^-1]_{s_k};  out_t = sum_k y_k (S^_k mod t) mod t   (no correction)
+//   ModUp      digit j (Q-limbs D_j) extended to every other limb of Q u P
+//   key-switch acc{0,1} = sum_j NTT(ModUp_j(INTT d2)) (.) evk{b,a}_j  over Q u P
+//   ModDown    out_i = (acc_i - NTT(baseconv_{P->Q}(INTT acc_P))_i) P^-1 mod q_i
+// Restated bit-exactly by oracle/fhe_oracle.c (oracle_baseconv / oracle_keyswitch).
+//
+// Every constant multiplier is a Shoup pair, so a conversion costs S + S*T Shoup products per
+// coefficient and no Barrett; partial sums stay in [0, 2t) by one conditional subtraction each.
+#include <algorithm>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace fhe {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxSrc = 16;
+
+// out row r -> ctx limb: r < n0 ? base0 + r : base1 + (r - n0)
+struct RowMap {
+  u32 n0, base0, base1;
+  __host__ __device__ u32 limb(u32 r) const { return r < n0 ? base0 + r : base1 + (r - n0); }
+};
+
+inline ulonglong2 shoup_pair(u64 w, u64 q) {
+  ulonglong2 p;
+  p.x = w;
+  p.y = (u64)(((u128)w << 64) / q);
+  return p;
+}
+
+// in: S rows (stride N) over ctx limbs src0..src0+S-1; out: T rows (stride N), row r over
+// ctx limb map.limb(r); rows whose limb lies in [skip_lo, skip_hi) are left untouched.
+// inv[k] = (S^_k)^-1 mod s_k; hat[k * hs + limb] = S^_k mod limb.
+template <int S>
+__global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ in, u32 src0,
+                                                       u64* __restrict__ out, u32 T, RowMap map,
+                                                       u32 skip_lo, u32 skip_hi, u64 n,
+                                                       const ulonglong2* __restrict__ inv,
+                                                       const ulonglong2* __restrict__ hat, u32 hs,
+                                                       const ModParams* __restrict__ mods) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  u64 y[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const u64 qk = mods[src0 + k].q;
+    const ulonglong2 w = inv[k];
+    y[k] = csub(shoup_lazy(in[(u64)k * n + i], w.x, w.y, qk), qk);
+  }
+  for (u32 r = 0; r < T; ++r) {
+    const u32 limb = map.limb(r);
+    if (limb >= skip_lo && limb < skip_hi) continue;
+    const u64 t = mods[limb].q, t2 = 2 * t;
+    u64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const ulonglong2 w = hat[(u64)k * hs + limb];
+      acc = csub(acc + shoup_lazy(y[k], w.x, w.y, t), t2);
+    }
+    out[(u64)r * n + i] = csub(acc, t);
+  }
+}
+
+// acc{0,1}[r][i] = sum_j e_j[r][i] * evk{b,a}[j][r][i] mod t, r over own Q-limbs then P-limbs.
+// e_j = d2_own row when row r's limb is in digit j, else ext[j] row (NTT form).
+__global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0,
+                                                       u64* __restrict__ acc1,
+                                                       const u64* __restrict__ ext,
+                                                       const u64* __restrict__ d2_own,
+                                                       const u64* __restrict__ evk_b,
+                                                       const u64* __restrict__ evk_a, u32 rows,
+                                                       RowMap map, u32 dnum, u32 alpha, u32 L,
+                                                       u64 n, const ModParams* __restrict__ mods) {
+  const u64 total = (u64)rows * n;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const u32 r = (u32)(e / n);
+    const u64 i = e % n;
+    const u32 limb = map.limb(r);
+    const ModParams m = mods[limb];
+    u64 s0 = 0, s1 = 0;
+    for (u32 j = 0; j < dnum; ++j) {
+      const bool own = limb < L && limb / alpha == j;
+      const u64 x = own ? d2_own[(u64)r * n + i] : ext[((u64)j * rows + r) * n + i];
+      const u64 off = ((u64)j * rows + r) * n + i;
+      s0 = csub(s0 + mulmod_barrett(x, evk_b[off], m), m.q);
+      s1 = csub(s1 + mulmod_barrett(x, evk_a[off], m), m.q);
+    }
+    acc0[e] = s0;
+    acc1[e] = s1;
+  }
+}
+
+// out{0,1}[r][i] = (acc{0,1}[r][i] - conv{0,1}[r][i]) * P^-1 mod q   (own Q-limbs)
+__global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ out0,
+                                                             u64* __restrict__ out1,
+                                                             const u64* __restrict__ acc0,
+                                                             const u64* __restrict__ acc1,
+                                                             u64 acc_pstride,
+                                                             const u64* __restrict__ conv, u32 rows,
+                                                             u32 limb0, u64 n,
+                                                             const ulonglong2* __restrict__ pinv,
+                                                             const ModParams* __restrict__ mods) {
+  const u64 total = (u64)rows * n;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const u32 limb = limb0 + (u32)(e / n);
+    const u64 q = mods[limb].q;
+    const ulonglong2 w = pinv[limb];
+    const u64 c0 = conv[e], c1 = conv[total + e];
+    const u64 x0 = acc0[e], x1 = acc1[e];
+    (void)acc_pstride;
+    out0[e] = csub(shoup_lazy(x0 + q - c0, w.x, w.y, q), q);
+    out1[e] = csub(shoup_lazy(x1 + q - c1, w.x, w.y, q), q);
+  }
+}
+
+template <class T>
+int upload(T** dptr, const std::vector<T>& v) {
+  if (v.empty()) return kOk;
+  FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(dptr), v.size() * sizeof(T)));
+  FHE_HIP_CHECK(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return kOk;
+}
+
+// (S^_k)^-1 mod s_k and S^_k mod t for a source set and every ctx limb t.
+void conv_tables(const std::vector<u64>& mods, u32 s0, u32 S, std::vector<ulonglong2>& inv,
+                 std::vector<ulonglong2>& hat) {
+  const u32 M = (u32)mods.size();
+  inv.resize(S);
+  hat.resize((size_t)S * M);
+  for (u32 k = 0; k < S; ++k) {
+    const u64 sk = mods[s0 + k];
+    u64 h = 1;
+    for (u32 i = 0; i < S; ++i)
+      if (i != k) h = mulmod_u64(h, mods[s0 + i] % sk, sk);
+    inv[k] = shoup_pair(powmod_u64(h, sk - 2, sk), sk);
+    for (u32 t = 0; t < M; ++t) {
+      const u64 tm = mods[t];
+      u64 hm = 1;
+      for (u32 i = 0; i < S; ++i)
+        if (i != k) hm = mulmod_u64(hm, mods[s0 + i] % tm, tm);
+      hat[(size_t)k * M + t] = shoup_pair(hm, tm);
+    }
+  }
+}
+
+template <int S>
+void launch_bc(const u64* in, u32 src0, u64* out, u32 T, RowMap map, u32 skip_lo, u32 skip_hi,
+               u64 n, const ulonglong2* inv, const ulonglong2* hat, u32 hs, const ModParams* mods,
+               hipStream_t s) {
+  const u32 g = (u32)((n + kThreads - 1) / kThreads);
+  k_baseconv<S><<<g, kThreads, 0, s>>>(in, src0, out, T, map, skip_lo, skip_hi, n, inv, hat, hs,
+                                       mods);
+}
+
+int baseconv_any(u32 S, const u64* in, u32 src0, u64* out, u32 T, RowMap map, u32 skip_lo,
+                 u32 skip_hi, u64 n, const ulonglong2* inv, const ulonglong2* hat, u32 hs,
+                 const ModParams* mods, hipStream_t s) {
+  switch (S) {
+#define X(k) \
+  case k:    \
+    launch_bc<k>(in, src0, out, T, map, skip_lo, skip_hi, n, inv, hat, hs, mods, s); break;
+    X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+#undef X
+    default:
+      set_error("baseconv: more than 16 source limbs");
+      return kUnsupported;
+  }
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+
+inline u32 grid_for(u64 work) {
+  const u64 blocks = (work + kThreads - 1) / kThreads;
+  return (u32)(blocks < 256 * 16 ? (blocks ? blocks : 1) : 256 * 16);
+}
+
+}  // namespace
+
+int build_rns_tables(fhe_ctx* c) {
+  if (c->K == 0) return kOk;
+  const u32 L = c->L, K = c->K, M = L + K, alpha = c->alpha;
+  if (alpha > (u32)kMaxSrc || K > (u32)kMaxSrc) {
+    set_error("ctx_create: key-switch needs alpha <= 16 and K <= 16");
+    return kUnsupported;
+  }
+  std::vector<ulonglong2> up_inv((size_t)c->dnum * alpha), up_hat((size_t)c->dnum * alpha * M);
+  for (u32 j = 0; j < c->dnum; ++j) {
+    const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
+    if (lo >= L) break;
+    std::vector<ulonglong2> inv, hat;
+    conv_tables(c->moduli, lo, hi - lo, inv, hat);
+    std::copy(inv.begin(), inv.end(), up_inv.begin() + (size_t)j * alpha);
+    std::copy(hat.begin(), hat.end(), up_hat.begin() + (size_t)j * alpha * M);
+  }
+  std::vector<ulonglong2> dn_inv, dn_hat, pinv(L);
+  conv_tables(c->moduli, L, K, dn_inv, dn_hat);
+  for (u32 i = 0; i < L; ++i) {
+    const u64 q = c->moduli[i];
+    u64 pm = 1;
+    for (u32 k = 0; k < K; ++k) pm = mulmod_u64(pm, c->moduli[L + k] % q, q);
+    pinv[i] = shoup_pair(powmod_u64(pm, q - 2, q), q);
+  }
+  int rc;
+  if ((rc = upload(&c->d_modup_inv, up_inv)) || (rc = upload(&c->d_modup_hat, up_hat)) ||
+      (rc = upload(&c->d_moddown_inv, dn_inv)) || (rc = upload(&c->d_moddown_hat, dn_hat)) ||
+      (rc = upload(&c->d_pinv, pinv)))
+    return rc;
+  return kOk;
+}
+
+size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs) {
+  const u64 rows = nlimbs + c->K;
+  // ext [dnum][rows][N] + acc0/acc1 [2][rows][N] + conv [2][nlimbs][N] + c_all [L][N]
+  return ((u64)c->dnum * rows + 2 * rows + 2 * nlimbs + c->L) * c->n * sizeof(u64);
+}
+
+int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_all,
+                           const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
+                           u32 nlimbs, void* ws, hipStream_t s) {
+  if (c->K == 0) {
+    set_error("keyswitch: context has no special primes (K = 0)");
+    return kInvalid;
+  }
+  const u32 L = c->L, K = c->K, M = L + K, alpha = c->alpha, rows = nlimbs + K;
+  const u64 n = c->n;
+  u64* ext = static_cast<u64*>(ws);
+  u64* acc = ext + (u64)c->dnum * rows * n;  // [2][rows][N]
+  u64* conv = acc + 2 * (u64)rows * n;       // [2][nlimbs][N]
+  const RowMap map{nlimbs, limb0, L};
+  int rc;
+  // ModUp + NTT, per digit, for every row not in the digit itself
+  for (u32 j = 0; j < c->dnum; ++j) {
+    const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
+    u64* e = ext + (u64)j * rows * n;
+    if ((rc = baseconv_any(hi - lo, c_all + (u64)lo * n, lo, e, rows, map, lo, hi, n,
+                           c->d_modup_inv + (size_t)j * alpha, c->d_modup_hat + (size_t)j * alpha * M,
+                           M, c->d_mods, s)))
+      return rc;
+    // own Q-limbs outside [lo, hi): up to two ranges, then the P-limbs
+    const u32 a0 = limb0, a1 = std::min(limb0 + nlimbs, lo);
+    if (a1 > a0 && (rc = launch_ntt(c, true, e, e, 1, 0, a0, a1 - a0, s))) return rc;
+    const u32 b0 = std::max(limb0, hi), b1 = limb0 + nlimbs;
+    if (b1 > b0 &&
+        (rc = launch_ntt(c, true, e + (u64)(b0 - limb0) * n, e + (u64)(b0 - limb0) * n, 1, 0, b0,
+                         b1 - b0, s)))
+      return rc;
+    if ((rc = launch_ntt(c, true, e + (u64)nlimbs * n, e + (u64)nlimbs * n, 1, 0, L, K, s)))
+      return rc;
+  }
+  k_ks_inner<<<grid_for((u64)rows * n), kThreads, 0, s>>>(acc, acc + (u64)rows * n, ext, d2_own,
+                                                          evk_b, evk_a, rows, map, c->dnum, alpha,
+                                                          L, n, c->d_mods);
+  FHE_HIP_CHECK(hipGetLastError());
+  // ModDown: INTT the P rows of both accumulators, convert P -> own Q-limbs, NTT, finish
+  u64* accp = acc + (u64)nlimbs * n;
+  if ((rc = launch_ntt(c, false, accp, accp, 2, (u64)rows * n, L, K, s))) return rc;
+  const RowMap qmap{nlimbs, limb0, 0};
+  for (int w = 0; w < 2; ++w) {
+    if ((rc = baseconv_any(K, accp + (u64)w * rows * n, L, conv + (u64)w * nlimbs * n, nlimbs,
+                           qmap, 0, 0, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, s)))
+      return rc;
+  }
+  if ((rc = launch_ntt(c, true, conv, conv, 2, (u64)nlimbs * n, limb0, nlimbs, s))) return rc;
+  // finish: acc rows [0, nlimbs) of acc0 / acc1
+  const u64 total = (u64)nlimbs * n;
+  // acc1 Q-rows live at acc + rows*n; pass via a compact copy-free view: two launches
+  k_moddown_finish<<<grid_for(total), kThreads, 0, s>>>(ks0, ks1, acc, acc + (u64)rows * n, 0,
+                                                        conv, nlimbs, limb0, n, c->d_pinv,
+                                                        c->d_mods);
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+
+int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u32 t0, u32 T,
+                    hipStream_t s) {
+  const u32 M = c->L + c->K;
+  if (S == 0 || T == 0 || s0 + S > M || t0 + T > M || (s0 < t0 + T && t0 < s0 + S)) {
+    set_error("baseconv: limb ranges out of bounds or overlapping");
+    return kInvalid;
+  }
+  std::vector<ulonglong2> inv, hat;
+  conv_tables(c->moduli, s0, S, inv, hat);
+  ulonglong2* d_tab = nullptr;
+  FHE_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d_tab), (inv.size() + hat.size()) * 16, s));
+  FHE_HIP_CHECK(hipMemcpyAsync(d_tab, inv.data(), inv.size() * 16, hipMemcpyHostToDevice, s));
+  FHE_HIP_CHECK(hipMemcpyAsync(d_tab + inv.size(), hat.data(), hat.size() * 16,
+                               hipMemcpyHostToDevice, s));
+  const int rc = baseconv_any(S, in, s0, out, T, RowMap{T, t0, 0}, 0, 0, c->n, d_tab,
+                              d_tab + inv.size(), M, c->d_mods, s);
+  // the host vectors must outlive the async copies
+  FHE_HIP_CHECK(hipStreamSynchronize(s));
+  FHE_HIP_CHECK(hipFreeAsync(d_tab, s));
+  return rc;
+}
+
+}  // namespace fhe

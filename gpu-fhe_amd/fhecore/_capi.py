@@ -1,0 +1,78 @@
+"""ctypes binding of libfhecore (include/fhecore.h).
+
+The library is built in-tree by ``make -C gpu-fhe_amd`` (``__graft_entry__.build()``) into
+``gpu-fhe_amd/lib/libfhecore.so``.  There is no fallback: if the shared object is missing or
+fails to load, every entry point raises -- the product path never silently computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libfhecore.so")
+
+FHE_OK = 0
+_ERRNAMES = {-1: "FHE_EINVAL", -2: "FHE_ENOMEM", -3: "FHE_EDEVICE", -4: "FHE_EUNSUPPORTED"}
+
+_u32, _u64, _i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+_vp = ctypes.c_void_p
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/fhecore.h one to one
+SIGNATURES = {
+    "fhe_last_error": (ctypes.c_char_p, []),
+    "fhe_version": (ctypes.c_char_p, []),
+    "fhe_gen_moduli": (_i32, [_u32, _u32, _u32, _u32, _u64p]),
+    "fhe_ctx_create": (_i32, [ctypes.POINTER(_vp), _u32, _u64p, _u32, _u64p, _u32, _u32, _i32]),
+    "fhe_ctx_destroy": (_i32, [_vp]),
+    "fhe_ctx_moduli": (_i32, [_vp, _u64p, _u64p]),
+    "fhe_ctx_shape": (_i32, [_vp, ctypes.POINTER(_u32), ctypes.POINTER(_u32),
+                             ctypes.POINTER(_u32), ctypes.POINTER(_u32), ctypes.POINTER(_i32)]),
+    "fhe_ctx_reserve": (_i32, [_vp, _sz]),
+    "fhe_vec_add": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]),
+    "fhe_vec_sub": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]),
+    "fhe_vec_mul": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]),
+    "fhe_vec_op_mod": (_i32, [_i32, _vp, _vp, _vp, _u64, _u64, _u64p, _u64, _i32, _i32, _vp]),
+    "fhe_ntt_fwd": (_i32, [_vp, _vp, _u32, _u32, _u32, _vp]),
+    "fhe_ntt_inv": (_i32, [_vp, _vp, _u32, _u32, _u32, _vp]),
+    "fhe_hommult_workspace": (_sz, [_vp, _u32, _u32]),
+    "fhe_hommult": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
+    "fhe_baseconv": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _vp]),
+    "fhe_keyswitch_workspace": (_sz, [_vp, _u32]),
+    "fhe_keyswitch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fhe_keyswitch_shard": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
+}
+
+_lib = None
+
+
+class FheError(RuntimeError):
+    """A libfhecore entry point returned a negative status."""
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FheError(f"libfhecore not built: {LIB_PATH} is missing "
+                           "(run `make -C gpu-fhe_amd` or __graft_entry__.build())")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != FHE_OK:
+        msg = load().fhe_last_error().decode(errors="replace")
+        raise FheError(f"{what} failed: {_ERRNAMES.get(rc, rc)}: {msg}")
+
+
+def u64_array(values):
+    arr = (ctypes.c_uint64 * len(values))(*[int(v) for v in values])
+    return arr

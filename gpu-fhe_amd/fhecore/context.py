@@ -1,0 +1,242 @@
+"""Context / Ciphertext / Evaluator: the host-side API over libfhecore.
+
+SURVEY.md §8b asks for a Context/Ciphertext/Evaluator layer above the C ABI (the reference has
+no such layer: it passes ``MOD`` per call, /root/reference/arithmetic.py:3-13).  Device memory,
+streams and multi-GPU collectives are PyTorch-ROCm plumbing; every arithmetic operation is a
+libfhecore call into hand-written gfx950 kernels.  Tensors are int64 views of the uint64
+residues, layout [..., limb, N], on a HIP device.
+"""
+from __future__ import annotations
+
+import ctypes
+from functools import lru_cache
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, load
+
+try:  # torch is the device-memory / stream provider
+    import torch
+except ImportError:  # pragma: no cover - the image always has torch
+    torch = None
+
+
+# ----------------------------------------------------------------------------- parameters
+
+@lru_cache(maxsize=None)
+def _gen_moduli_cached(log_n: int, count: int, bits: int, skip: int) -> tuple:
+    out = (ctypes.c_uint64 * count)()
+    check(load().fhe_gen_moduli(log_n, count, bits, skip, out), "fhe_gen_moduli")
+    return tuple(int(v) for v in out)
+
+
+def gen_moduli(log_n: int, count: int, bits: int = 60, skip: int = 0) -> list:
+    """SURVEY.md §8a' modulus chain: the largest primes < 2^bits, q = 1 mod 2N, descending."""
+    return list(_gen_moduli_cached(log_n, count, bits, skip))
+
+
+def default_params(log_n: int, L: int, K: int = 0):
+    """(Q-moduli, P-moduli): L + K consecutive primes of the §8a' chain."""
+    m = gen_moduli(log_n, L + K)
+    return m[:L], m[L:]
+
+
+# ----------------------------------------------------------------------------- device helpers
+
+def _require_device():
+    if torch is None or not torch.cuda.is_available():
+        raise _capi.FheError("fhecore needs a HIP device (torch.cuda.is_available() is False); "
+                             "there is no CPU fallback")
+
+
+def to_device(x, device=None):
+    """numpy uint64/int64 (or any integer array with values in [0, 2^64)) -> int64 device tensor."""
+    _require_device()
+    if isinstance(x, torch.Tensor):
+        return x.to(device or "cuda").contiguous()
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
+    return torch.from_numpy(a.view(np.int64)).to(device or "cuda")
+
+
+def to_host(t) -> np.ndarray:
+    """int64 device tensor -> numpy uint64 array."""
+    return t.detach().to("cpu").contiguous().numpy().view(np.uint64)
+
+
+def _ptr(t) -> int:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _check_tensor(t, what, shape_tail=None):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{what}: expected a HIP device tensor")
+    if t.dtype not in (torch.int64, torch.uint64):
+        raise TypeError(f"{what}: expected int64/uint64 residues, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+    if shape_tail is not None and tuple(t.shape[-len(shape_tail):]) != tuple(shape_tail):
+        raise ValueError(f"{what}: trailing shape {tuple(t.shape)} != (..., {shape_tail})")
+
+
+# ----------------------------------------------------------------------------- context
+
+class Context:
+    """RNS-CKKS-style parameter context on one HIP device (wraps ``fhe_ctx``).
+
+    moduli: Q-primes (L of them); special: P-primes (K, for key-switching); dnum gadget digits.
+    Defaults follow SURVEY.md §8a' (``default_params``).
+    """
+
+    def __init__(self, log_n: int, moduli=None, special=None, dnum: int = 1, L: int = None,
+                 K: int = 0, device: int = None):
+        _require_device()
+        lib = load()
+        if moduli is None:
+            if L is None:
+                raise ValueError("give moduli or L")
+            moduli, dflt_special = default_params(log_n, L, K)
+            if special is None:
+                special = dflt_special
+        special = list(special or [])
+        moduli = [int(q) for q in moduli]
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.log_n = int(log_n)
+        self.n = 1 << self.log_n
+        self.L, self.K = len(moduli), len(special)
+        self.dnum = int(dnum) if self.K else 0
+        self.alpha = -(-self.L // self.dnum) if self.K else 0
+        self._ptr = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.fhe_ctx_create(ctypes.byref(self._ptr), self.log_n, _capi.u64_array(moduli),
+                                     self.L, _capi.u64_array(special) if special else None,
+                                     self.K, self.dnum, self.device), "fhe_ctx_create")
+        mods = (ctypes.c_uint64 * (self.L + self.K))()
+        psi = (ctypes.c_uint64 * (self.L + self.K))()
+        check(lib.fhe_ctx_moduli(self._ptr, mods, psi), "fhe_ctx_moduli")
+        self.moduli = [int(v) for v in mods][: self.L]
+        self.special = [int(v) for v in mods][self.L:]
+        self.psi = [int(v) for v in psi]
+
+    # -- lifetime
+    def close(self):
+        if getattr(self, "_ptr", None) and self._ptr.value:
+            load().fhe_ctx_destroy(self._ptr)
+            self._ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._ptr
+
+    @property
+    def all_moduli(self):
+        return self.moduli + self.special
+
+    def _dev(self):
+        return torch.device("cuda", self.device)
+
+    def empty(self, *shape):
+        return torch.empty(shape, dtype=torch.int64, device=self._dev())
+
+    def workspace(self, nbytes: int):
+        return torch.empty((max(int(nbytes), 8) + 7) // 8, dtype=torch.int64, device=self._dev())
+
+    # -- NTT (replaces NTT / iNTT, arithmetic.py:15-19)
+    def ntt_(self, t, limb0: int = 0):
+        """In-place forward NTT of a [..., nlimbs, N] tensor (limb l uses modulus limb0 + l)."""
+        return self._ntt(t, limb0, True)
+
+    def intt_(self, t, limb0: int = 0):
+        return self._ntt(t, limb0, False)
+
+    def _ntt(self, t, limb0, fwd):
+        _check_tensor(t, "ntt", (self.n,))
+        nl = t.shape[-2] if t.dim() >= 2 else 1
+        polys = t.numel() // (nl * self.n)
+        fn = load().fhe_ntt_fwd if fwd else load().fhe_ntt_inv
+        with torch.cuda.device(self.device):
+            check(fn(self._ptr, _ptr(t), polys, limb0, nl, _stream(t)), fn.__name__)
+        return t
+
+    # -- coefficient-wise ops (replace vec_add / vec_sub / vec_mul, arithmetic.py:3-13)
+    def vec(self, op: str, a, b, out=None, limb0: int = 0):
+        _check_tensor(a, op, (self.n,))
+        _check_tensor(b, op, (self.n,))
+        if a.shape != b.shape:
+            raise AssertionError("a.shape != b.shape")  # the reference asserts (arithmetic.py:4)
+        out = torch.empty_like(a) if out is None else out
+        nl = a.shape[-2] if a.dim() >= 2 else 1
+        polys = a.numel() // (nl * self.n)
+        fn = {"add": load().fhe_vec_add, "sub": load().fhe_vec_sub, "mul": load().fhe_vec_mul}[op]
+        with torch.cuda.device(self.device):
+            check(fn(self._ptr, _ptr(out), _ptr(a), _ptr(b), polys, limb0, nl, _stream(a)),
+                  fn.__name__)
+        return out
+
+    # -- HomMult (SURVEY.md §8a')
+    def hommult(self, a, b, out=None, limb0: int = 0, workspace=None):
+        """a, b: [batch, 2, nlimbs, N] (or [2, nlimbs, N]) coefficient form -> [batch, 3, nlimbs, N]."""
+        _check_tensor(a, "hommult", (self.n,))
+        _check_tensor(b, "hommult", (self.n,))
+        if a.shape != b.shape or a.shape[-3] != 2:
+            raise ValueError("hommult: a, b must both be [batch, 2, nlimbs, N]")
+        squeeze = a.dim() == 3
+        batch = 1 if squeeze else a.shape[0]
+        nl = a.shape[-2]
+        shape = (3, nl, self.n) if squeeze else (batch, 3, nl, self.n)
+        out = self.empty(*shape) if out is None else out
+        lib = load()
+        ws = workspace
+        if ws is None:
+            ws = self.workspace(lib.fhe_hommult_workspace(self._ptr, batch, nl))
+        with torch.cuda.device(self.device):
+            check(lib.fhe_hommult(self._ptr, _ptr(out), _ptr(a), _ptr(b), batch, limb0, nl,
+                                  _ptr(ws), _stream(a)), "fhe_hommult")
+        return out
+
+    # -- base conversion / key-switch (SURVEY.md §8a')
+    def baseconv(self, x, s0: int, t0: int, T: int):
+        _check_tensor(x, "baseconv", (self.n,))
+        S = x.shape[-2]
+        out = self.empty(T, self.n)
+        with torch.cuda.device(self.device):
+            check(load().fhe_baseconv(self._ptr, _ptr(out), _ptr(x), s0, S, t0, T, _stream(x)),
+                  "fhe_baseconv")
+        return out
+
+    def keyswitch(self, d2, evk_b, evk_a, workspace=None):
+        """d2 [L, N] NTT form; evk_b/evk_a [dnum, L + K, N] NTT form -> (ks0, ks1) [L, N] NTT form."""
+        for t, nm in ((d2, "d2"), (evk_b, "evk_b"), (evk_a, "evk_a")):
+            _check_tensor(t, nm, (self.n,))
+        if tuple(evk_b.shape) != (self.dnum, self.L + self.K, self.n) or evk_a.shape != evk_b.shape:
+            raise ValueError("keyswitch: evk must be [dnum, L + K, N]")
+        ks0, ks1 = self.empty(self.L, self.n), self.empty(self.L, self.n)
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_keyswitch_workspace(self._ptr, self.L))
+        with torch.cuda.device(self.device):
+            check(lib.fhe_keyswitch(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(d2), _ptr(evk_b),
+                                    _ptr(evk_a), _ptr(ws), _stream(d2)), "fhe_keyswitch")
+        return ks0, ks1
+
+    def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0: int, workspace=None):
+        nl = d2_own.shape[-2]
+        ks0, ks1 = self.empty(nl, self.n), self.empty(nl, self.n)
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_keyswitch_workspace(self._ptr, nl))
+        with torch.cuda.device(self.device):
+            check(lib.fhe_keyswitch_shard(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(c_all),
+                                          _ptr(d2_own), _ptr(evk_b), _ptr(evk_a), limb0, nl,
+                                          _ptr(ws), _stream(d2_own)), "fhe_keyswitch_shard")
+        return ks0, ks1

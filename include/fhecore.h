@@ -1,0 +1,139 @@
+/* libfhecore -- MI355X-native (gfx950) FHE polynomial-arithmetic core: C ABI.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * (Kelly-Zhe/GPU-FHE @ 2025-02-12) is a Python/numpy module whose whole operator surface is
+ *     vec_add(a, b, MOD)   /root/reference/arithmetic.py:3-5
+ *     vec_sub(a, b, MOD)   /root/reference/arithmetic.py:7-9
+ *     vec_mul(a, b, MOD)   /root/reference/arithmetic.py:11-13   (= poly_mul_pointwise)
+ *     NTT(x), iNTT(x)      /root/reference/arithmetic.py:15-19   (identity stubs there)
+ *     poly_add(a, b, MOD)  /root/reference/ polynomial.py:3-5
+ * Each entry point below names the reference function it replaces; the Python shim in
+ * gpu-fhe_amd/arithmetic.py and gpu-fhe_amd/polynomial.py binds them by ctypes under the
+ * reference's own names.  Components the north star names but the
+ * reference lacks (Shoup/Barrett modmul, RNS base conversion, key-switch, HomMult) follow
+ * the build-defined spec of SURVEY.md §8a'.
+ *
+ * Conventions
+ *  - Return 0 on success, a negative FHE_E* code on error; fhe_last_error() (thread-local)
+ *    describes the last failure.  No entry point aborts or throws.
+ *  - Every data pointer is DEVICE memory owned by the caller.  Residues are uint64 in
+ *    layout [poly][limb][N] (limb-major, each limb's N coefficients contiguous).
+ *  - `stream` is a hipStream_t (NULL = the legacy default stream).  Launches are
+ *    asynchronous and capture-safe (no allocation or synchronisation inside) unless noted.
+ *  - A context is immutable after creation: calls on different streams may share it, except
+ *    that passing workspace == NULL uses the context's internal workspace (not thread-safe).
+ *  - limb0 / nlimbs select a contiguous window of the context's Q-limbs (RNS-limb sharding).
+ */
+#ifndef FHECORE_H
+#define FHECORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FHE_OK 0
+#define FHE_EINVAL (-1)
+#define FHE_ENOMEM (-2)
+#define FHE_EDEVICE (-3)
+#define FHE_EUNSUPPORTED (-4)
+
+typedef struct fhe_ctx fhe_ctx;
+typedef void* fhe_stream_t; /* hipStream_t */
+
+/* Thread-local description of the last error ("" if none). */
+const char* fhe_last_error(void);
+/* Library version string. */
+const char* fhe_version(void);
+
+/* ---- parameters (host only) -------------------------------------------------------- */
+/* The `count` largest primes q < 2^bits with q = 1 (mod 2^(log_n+1)), descending, after skipping
+ * `skip` (SURVEY.md §8a' modulus chain; special primes P continue the same list). */
+int fhe_gen_moduli(uint32_t log_n, uint32_t count, uint32_t bits, uint32_t skip, uint64_t* out);
+
+/* ---- context ------------------------------------------------------------------------ */
+/* Creates a context on HIP device `device` for ring degree N = 2^log_n (10 <= log_n <= 17) with
+ * Q-primes q[0..L) and special primes p[0..K) (K may be 0: no key-switch) and dnum gadget digits.
+ * Every modulus must be a distinct prime < 2^61 with q = 1 (mod 2N).
+ * Precomputes psi^brv twiddles (psi = g^((q-1)/2N), g the smallest primitive root), Shoup
+ * companions, Barrett constants and key-switch base-conversion tables; uploads them.
+ * Replaces: nothing in the reference (it passes MOD per call, arithmetic.py:3). */
+int fhe_ctx_create(fhe_ctx** ctx, uint32_t log_n, const uint64_t* q, uint32_t L,
+                   const uint64_t* p, uint32_t K, uint32_t dnum, int device);
+int fhe_ctx_destroy(fhe_ctx* ctx);
+/* Copies the L + K moduli (Q then P) and their psi roots to host arrays (either may be NULL). */
+int fhe_ctx_moduli(const fhe_ctx* ctx, uint64_t* moduli, uint64_t* psi);
+/* log_n, L, K, dnum, device. */
+int fhe_ctx_shape(const fhe_ctx* ctx, uint32_t* log_n, uint32_t* L, uint32_t* K, uint32_t* dnum,
+                  int* device);
+/* Grows the context's internal workspace to >= bytes (allocates; not capture-safe). */
+int fhe_ctx_reserve(fhe_ctx* ctx, size_t bytes);
+
+/* ---- coefficient-wise ops on canonical residues ------------------------------------- */
+/* out = (a op b) mod q_{limb0 + l} for every poly and limb l in [0, nlimbs); inputs in [0, q).
+ * out may alias a or b.  Replaces vec_add / vec_sub / vec_mul (arithmetic.py:3-13) and
+ * poly_add (' polynomial.py':3-5, with polys = 2). */
+int fhe_vec_add(const fhe_ctx* ctx, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                uint32_t polys, uint32_t limb0, uint32_t nlimbs, fhe_stream_t stream);
+int fhe_vec_sub(const fhe_ctx* ctx, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                uint32_t polys, uint32_t limb0, uint32_t nlimbs, fhe_stream_t stream);
+int fhe_vec_mul(const fhe_ctx* ctx, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                uint32_t polys, uint32_t limb0, uint32_t nlimbs, fhe_stream_t stream);
+
+/* Generic form used by the reference-shaped Python API: a, b, out are rows x cols matrices;
+ * row r uses modulus mods[r * mod_stride] (mod_stride 0 = one scalar MOD).  `mods` is a HOST
+ * array; inputs may be any uint64 (signed_in = 1: any int64), moduli any value in [2, 2^64).
+ * Result = Python's exact (a op b) % MOD.  op: 0 add, 1 sub, 2 mul.
+ * Allocates a small stream-ordered table (not capture-safe). */
+int fhe_vec_op_mod(int op, uint64_t* out, const uint64_t* a, const uint64_t* b, uint64_t rows,
+                   uint64_t cols, const uint64_t* mods, uint64_t mod_stride, int signed_in,
+                   int device, fhe_stream_t stream);
+
+/* ---- negacyclic NTT ------------------------------------------------------------------ */
+/* In place on data [polys][nlimbs][N]; limb l uses q_{limb0 + l} (limb0 + nlimbs <= L + K, so
+ * P-limbs are addressable too).  Forward: natural -> bit-reversed order,
+ * NTT(a)[k] = sum_i a_i psi^((2 brv(k) + 1) i); inverse: exact inverse incl. N^-1.
+ * Inputs canonical in [0, q); outputs canonical.  Replaces NTT / iNTT (arithmetic.py:15-19). */
+int fhe_ntt_fwd(const fhe_ctx* ctx, uint64_t* data, uint32_t polys, uint32_t limb0,
+                uint32_t nlimbs, fhe_stream_t stream);
+int fhe_ntt_inv(const fhe_ctx* ctx, uint64_t* data, uint32_t polys, uint32_t limb0,
+                uint32_t nlimbs, fhe_stream_t stream);
+
+/* ---- ct x ct homomorphic multiplication (tensor) ----------------------------------------
+ * a, b: [batch][2][nlimbs][N] coefficient form; d: [batch][3][nlimbs][N] coefficient form with
+ * d0 = a0 b0, d1 = a0 b1 + a1 b0, d2 = a1 b1 in Z_q[X]/(X^N + 1) (NTT -> pointwise -> INTT).
+ * workspace: >= fhe_hommult_workspace(ctx, batch, nlimbs) bytes of device memory, or NULL.
+ * Replaces the caller-composed NTT -> vec_mul/vec_add -> iNTT chain (SURVEY.md §3 stack 4). */
+size_t fhe_hommult_workspace(const fhe_ctx* ctx, uint32_t batch, uint32_t nlimbs);
+int fhe_hommult(const fhe_ctx* ctx, uint64_t* d, const uint64_t* a, const uint64_t* b,
+                uint32_t batch, uint32_t limb0, uint32_t nlimbs, void* workspace,
+                fhe_stream_t stream);
+
+/* ---- RNS base conversion ---------------------------------------------------------------
+ * Fast basis extension (no correction) from ctx limbs [s0, s0+S) to [t0, t0+T) (disjoint),
+ * coefficient domain: in [S][N] -> out [T][N].  S <= 16.  Synchronises `stream`. */
+int fhe_baseconv(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t s0, uint32_t S,
+                 uint32_t t0, uint32_t T, fhe_stream_t stream);
+
+/* ---- hybrid key-switch (relinearisation) -------------------------------------------------
+ * Single-device form: d2 [L][N] NTT form over Q; evk_b, evk_a [dnum][L + K][N] NTT form over
+ * Q u P; ks0, ks1 [L][N] NTT form: ks0 + ks1 s = d2 s'' + small (SURVEY.md §8a').
+ * Sharded form (one rank of G): c_all [L][N] = INTT(d2) all-gathered (coefficient form),
+ * d2_own [nlimbs][N] NTT form of Q-limbs [limb0, limb0 + nlimbs), evk slices
+ * [dnum][nlimbs + K][N] (own Q-limbs then all K P-limbs); outputs [nlimbs][N].  The sharded
+ * outputs of G ranks concatenate to the single-device result bit for bit. */
+size_t fhe_keyswitch_workspace(const fhe_ctx* ctx, uint32_t nlimbs);
+int fhe_keyswitch(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const uint64_t* d2,
+                  const uint64_t* evk_b, const uint64_t* evk_a, void* workspace,
+                  fhe_stream_t stream);
+int fhe_keyswitch_shard(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const uint64_t* c_all,
+                        const uint64_t* d2_own, const uint64_t* evk_b, const uint64_t* evk_a,
+                        uint32_t limb0, uint32_t nlimbs, void* workspace, fhe_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FHECORE_H */

@@ -1,0 +1,450 @@
+"""CPU math oracle for the FHE polynomial-arithmetic hot path (TEST INFRASTRUCTURE ONLY).
+
+This module is the checker, never the product: only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import it.  The shipped path lives in
+``gpu-fhe_amd/`` and runs hand-written HIP kernels; it never routes through this file.
+
+What it restates
+----------------
+* ``vec_add`` / ``vec_sub`` / ``vec_mul``: the reference's coefficient-wise modular ops,
+  ``/root/reference/arithmetic.py:3-13`` (``(a op b) % MOD``), with EXACT semantics -- the
+  values the reference produces on ``dtype=object`` inputs.  Pinned by the golden vectors in
+  ``tests/golden/`` that ``tests/golden/make_golden.py`` captured by importing the reference.
+* ``NTT`` / ``iNTT``: the reference's are identities (``arithmetic.py:15-19``), so their
+  parity is UNPINNED BY THE REFERENCE.  The build-defined spec (SURVEY.md §8a') is restated
+  here twice -- as the O(N^2) defining sum and as the Cooley-Tukey / Gentleman-Sande loops --
+  and the two are checked against each other and against a schoolbook negacyclic product.
+* HomMult, RNS fast base conversion, ModUp / ModDown and the hybrid key-switch:
+  absent from the reference; restated from SURVEY.md §8a'.
+
+Everything is exact Python-int arithmetic; numpy object arrays vectorise the small cases.
+"""
+from __future__ import annotations
+
+import math
+import random
+from functools import lru_cache
+
+import numpy as np
+
+# --------------------------------------------------------------------------------------
+# number theory
+# --------------------------------------------------------------------------------------
+
+_MR_BASES = (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37)
+
+
+def is_prime(n: int) -> bool:
+    """Deterministic Miller-Rabin for n < 3.3e24 (covers every 64-bit modulus)."""
+    if n < 2:
+        return False
+    for p in _MR_BASES:
+        if n % p == 0:
+            return n == p
+    d, s = n - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        s += 1
+    for a in _MR_BASES:
+        x = pow(a, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(s - 1):
+            x = x * x % n
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def _pollard_rho(n: int) -> int:
+    if n % 2 == 0:
+        return 2
+    rng = random.Random(n)
+    while True:
+        c = rng.randrange(1, n)
+        x = y = rng.randrange(2, n)
+        d = 1
+        while d == 1:
+            x = (x * x + c) % n
+            y = (y * y + c) % n
+            y = (y * y + c) % n
+            d = math.gcd(abs(x - y), n)
+        if d != n:
+            return d
+
+
+def factorize(n: int) -> dict:
+    """Prime factorisation {p: e} (Pollard rho + Miller-Rabin)."""
+    out: dict = {}
+    stack = [n]
+    while stack:
+        m = stack.pop()
+        if m == 1:
+            continue
+        if is_prime(m):
+            out[m] = out.get(m, 0) + 1
+            continue
+        for p in (2, 3, 5, 7, 11, 13):
+            if m % p == 0:
+                stack += [p, m // p]
+                break
+        else:
+            d = _pollard_rho(m)
+            stack += [d, m // d]
+    return out
+
+
+@lru_cache(maxsize=None)
+def primitive_root(q: int) -> int:
+    """Smallest generator of (Z/qZ)^* (SURVEY.md §8a': g = smallest primitive root)."""
+    fs = list(factorize(q - 1))
+    g = 2
+    while True:
+        if all(pow(g, (q - 1) // f, q) != 1 for f in fs):
+            return g
+        g += 1
+
+
+@lru_cache(maxsize=None)
+def psi_for(q: int, n: int) -> int:
+    """psi = g^((q-1)/2N) mod q: a primitive 2N-th root of unity (SURVEY.md §8a')."""
+    assert (q - 1) % (2 * n) == 0, "q must be 1 mod 2N"
+    psi = pow(primitive_root(q), (q - 1) // (2 * n), q)
+    assert pow(psi, n, q) == q - 1
+    return psi
+
+
+def gen_moduli(log_n: int, count: int, bits: int = 60, skip: int = 0) -> list:
+    """The ``count`` largest primes q < 2^bits with q = 1 (mod 2N), descending, after skipping
+    the first ``skip`` (SURVEY.md §8a': "the largest primes below 2^60, in descending order";
+    special primes P continue the same list)."""
+    step = 2 << log_n
+    q = ((1 << bits) - 1) // step * step + 1
+    if q >= (1 << bits):
+        q -= step
+    out = []
+    while len(out) < count + skip:
+        if is_prime(q):
+            out.append(q)
+        q -= step
+        assert q > step, "ran out of NTT primes"
+    return out[skip:]
+
+
+def bitrev(x: int, bits: int) -> int:
+    r = 0
+    for _ in range(bits):
+        r = (r << 1) | (x & 1)
+        x >>= 1
+    return r
+
+
+@lru_cache(maxsize=None)
+def twiddles(q: int, log_n: int):
+    """(psi_brv, psi_inv_brv, n_inv): psi_brv[k] = psi^brv(k), psi_inv_brv[k] = psi^-brv(k)."""
+    n = 1 << log_n
+    psi = psi_for(q, n)
+    psi_inv = pow(psi, q - 2, q)
+    pw = [1] * n
+    pwi = [1] * n
+    for i in range(1, n):
+        pw[i] = pw[i - 1] * psi % q
+        pwi[i] = pwi[i - 1] * psi_inv % q
+    brv = [bitrev(k, log_n) for k in range(n)]
+    return [pw[b] for b in brv], [pwi[b] for b in brv], pow(n, q - 2, q)
+
+
+# --------------------------------------------------------------------------------------
+# reference operators, exact semantics (arithmetic.py:3-13, ' polynomial.py':3-5)
+# --------------------------------------------------------------------------------------
+
+def _obj(x):
+    return np.asarray(x).astype(object)
+
+
+def vec_add(a, b, mod):
+    """(a + b) % MOD, exact -- arithmetic.py:3-5 on dtype=object."""
+    assert np.shape(a) == np.shape(b)
+    return (_obj(a) + _obj(b)) % _obj(mod)
+
+
+def vec_sub(a, b, mod):
+    """(a - b) % MOD, exact (Python floor-mod: result in [0, MOD)) -- arithmetic.py:7-9."""
+    assert np.shape(a) == np.shape(b)
+    return (_obj(a) - _obj(b)) % _obj(mod)
+
+
+def vec_mul(a, b, mod):
+    """(a * b) % MOD, exact -- arithmetic.py:11-13 (= poly_mul_pointwise in the NTT domain)."""
+    assert np.shape(a) == np.shape(b)
+    return (_obj(a) * _obj(b)) % _obj(mod)
+
+
+def poly_add(a, b, mod):
+    """Intended result of ' polynomial.py':3-5 (the reference discards it and returns None)."""
+    return vec_add(a[0], b[0], mod), vec_add(a[1], b[1], mod)
+
+
+# --------------------------------------------------------------------------------------
+# negacyclic NTT (SURVEY.md §8a')
+# --------------------------------------------------------------------------------------
+
+def ntt_naive(a, q: int):
+    """Defining sum: NTT(a)[k] = sum_i a_i psi^((2 brv(k) + 1) i) mod q. O(N^2)."""
+    n = len(a)
+    log_n = n.bit_length() - 1
+    psi = psi_for(q, n)
+    a = [int(v) for v in a]
+    out = []
+    for k in range(n):
+        root = pow(psi, 2 * bitrev(k, log_n) + 1, q)
+        acc, w = 0, 1
+        for ai in a:
+            acc += ai * w
+            w = w * root % q
+        out.append(acc % q)
+    return out
+
+
+def ntt_fwd(a, q: int):
+    """Cooley-Tukey, natural in -> bit-reversed out (SEAL / Longa-Naehrig loop)."""
+    a = [int(v) for v in a]
+    n = len(a)
+    tw, _, _ = twiddles(q, n.bit_length() - 1)
+    t, m = n, 1
+    while m < n:
+        t //= 2
+        for i in range(m):
+            s = tw[m + i]
+            j1 = 2 * i * t
+            for j in range(j1, j1 + t):
+                u, v = a[j], a[j + t] * s % q
+                a[j], a[j + t] = (u + v) % q, (u - v) % q
+        m *= 2
+    return a
+
+
+def ntt_inv(a, q: int):
+    """Gentleman-Sande, bit-reversed in -> natural out, times N^-1."""
+    a = [int(v) for v in a]
+    n = len(a)
+    _, twi, n_inv = twiddles(q, n.bit_length() - 1)
+    t, m = 1, n
+    while m > 1:
+        h = m // 2
+        j1 = 0
+        for i in range(h):
+            s = twi[h + i]
+            for j in range(j1, j1 + t):
+                u, v = a[j], a[j + t]
+                a[j], a[j + t] = (u + v) % q, (u - v) * s % q
+            j1 += 2 * t
+        t *= 2
+        m = h
+    return [x * n_inv % q for x in a]
+
+
+def ntt_fwd_np(a, q: int):
+    """Vectorised (numpy object) form of ntt_fwd: same butterflies, stage at a time."""
+    n = len(a)
+    log_n = n.bit_length() - 1
+    tw = np.array(twiddles(q, log_n)[0], dtype=object)
+    x = np.array([int(v) for v in a], dtype=object)
+    for s in range(log_n):
+        m, t = 1 << s, n >> (s + 1)
+        x = x.reshape(m, 2, t)
+        w = tw[m:2 * m].reshape(m, 1)
+        u, v = x[:, 0, :], x[:, 1, :] * w % q
+        x = np.stack([(u + v) % q, (u - v) % q], axis=1)
+    return x.reshape(n)
+
+
+def ntt_inv_np(a, q: int):
+    n = len(a)
+    log_n = n.bit_length() - 1
+    _, twi, n_inv = twiddles(q, log_n)
+    twi = np.array(twi, dtype=object)
+    x = np.array([int(v) for v in a], dtype=object)
+    for s in range(log_n - 1, -1, -1):
+        m, t = 1 << s, n >> (s + 1)
+        x = x.reshape(m, 2, t)
+        w = twi[m:2 * m].reshape(m, 1)
+        u, v = x[:, 0, :], x[:, 1, :]
+        x = np.stack([(u + v) % q, (u - v) * w % q], axis=1)
+    return x.reshape(n) * n_inv % q
+
+
+def negacyclic_mul(a, b, q: int):
+    """Schoolbook product in Z_q[X]/(X^N + 1)."""
+    n = len(a)
+    a = np.array([int(v) for v in a], dtype=object)
+    b = [int(v) for v in b]
+    out = np.zeros(n, dtype=object)
+    for j, bj in enumerate(b):
+        if bj == 0:
+            continue
+        rolled = np.concatenate([-a[n - j:], a[:n - j]]) if j else a
+        out = out + rolled * bj
+    return out % q
+
+
+# --------------------------------------------------------------------------------------
+# RNS polynomials: arrays shaped [..., limb, N] (limb-major, SURVEY.md §2 kernel inventory)
+# --------------------------------------------------------------------------------------
+
+def rns_ntt_fwd(x, moduli):
+    x = np.asarray(x)
+    out = np.empty(x.shape, dtype=object)
+    for idx in np.ndindex(*x.shape[:-1]):
+        out[idx] = ntt_fwd_np(x[idx], moduli[idx[-1]])
+    return out
+
+
+def rns_ntt_inv(x, moduli):
+    x = np.asarray(x)
+    out = np.empty(x.shape, dtype=object)
+    for idx in np.ndindex(*x.shape[:-1]):
+        out[idx] = ntt_inv_np(x[idx], moduli[idx[-1]])
+    return out
+
+
+def _mods_col(moduli):
+    return np.array([int(q) for q in moduli], dtype=object).reshape(-1, 1)
+
+
+def hommult(a, b, moduli):
+    """ct x ct tensor (SURVEY.md §8a'): a, b = (2, L, N) coefficient form -> (3, L, N).
+    d0 = A0 B0, d1 = A0 B1 + A1 B0, d2 = A1 B1 (NTT domain, per limb), then INTT."""
+    qs = _mods_col(moduli)
+    A = rns_ntt_fwd(a, moduli)
+    B = rns_ntt_fwd(b, moduli)
+    d0 = A[0] * B[0] % qs
+    d1 = (A[0] * B[1] + A[1] * B[0]) % qs
+    d2 = A[1] * B[1] % qs
+    return rns_ntt_inv(np.stack([d0, d1, d2]), moduli)
+
+
+def baseconv(x, src, dst):
+    """Fast basis extension without correction (SURVEY.md §8a'), coefficient domain.
+    x: (len(src), N). y_i = [x_i * (S/s_i)^-1]_{s_i}; out_t = sum_i y_i * ((S/s_i) mod t) mod t."""
+    src = [int(s) for s in src]
+    S = math.prod(src)
+    x = np.asarray(x).astype(object)
+    ys = []
+    for i, s in enumerate(src):
+        hat = S // s
+        ys.append(x[i] * pow(hat % s, -1, s) % s)
+    out = []
+    for t in dst:
+        t = int(t)
+        acc = np.zeros(x.shape[-1], dtype=object)
+        for i, s in enumerate(src):
+            acc = acc + ys[i] * ((S // s) % t)
+        out.append(acc % t)
+    return np.stack(out)
+
+
+def digit_ranges(L: int, dnum: int):
+    """Limb ranges of the dnum gadget digits: alpha = ceil(L / dnum) limbs each (last may be short)."""
+    alpha = -(-L // dnum)
+    return [(j * alpha, min(L, (j + 1) * alpha)) for j in range(dnum) if j * alpha < L]
+
+
+def modup(c, qs, ps, dnum):
+    """c: (L, N) coefficient form over Q. Returns [dnum] arrays of shape (L + K, N): digit j
+    extended from its limbs D_j to every limb of Q u P (own limbs copied)."""
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    allm = qs + ps
+    out = []
+    for lo, hi in digit_ranges(len(qs), dnum):
+        dj = qs[lo:hi]
+        others = [i for i in range(len(allm)) if not lo <= i < hi]
+        conv = baseconv(c[lo:hi], dj, [allm[i] for i in others])
+        ext = np.empty((len(allm), c.shape[-1]), dtype=object)
+        ext[lo:hi] = np.asarray(c[lo:hi]).astype(object)
+        for k, i in enumerate(others):
+            ext[i] = conv[k]
+        out.append(ext)
+    return out
+
+
+def moddown_ntt(acc, qs, ps):
+    """acc: (L + K, N) NTT form over Q u P -> (L, N) NTT form over Q:
+    out = (acc_Q - NTT(conv_{P->Q}(INTT(acc_P)))) * P^-1 mod q_i."""
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    L = len(qs)
+    xp = rns_ntt_inv(np.asarray(acc[L:]), ps)
+    conv = baseconv(xp, ps, qs)
+    convn = rns_ntt_fwd(conv, qs)
+    P = math.prod(ps)
+    out = []
+    for i, q in enumerate(qs):
+        out.append((acc[i] - convn[i]) * pow(P % q, -1, q) % q)
+    return np.stack(out)
+
+
+def keyswitch(d2_ntt, evk_b, evk_a, qs, ps, dnum):
+    """Hybrid key-switch (SURVEY.md §8a'): d2 (L, N) NTT form over Q; evk_b/evk_a (dnum, L+K, N)
+    NTT form over Q u P.  Returns (ks0, ks1), each (L, N) NTT form over Q."""
+    allm = list(qs) + list(ps)
+    c = rns_ntt_inv(d2_ntt, qs)
+    ext = modup(c, qs, ps, dnum)
+    mods = _mods_col(allm)
+    acc0 = np.zeros((len(allm), c.shape[-1]), dtype=object)
+    acc1 = np.zeros_like(acc0)
+    for j, e in enumerate(ext):
+        en = rns_ntt_fwd(e, allm)
+        acc0 = (acc0 + en * np.asarray(evk_b[j]).astype(object)) % mods
+        acc1 = (acc1 + en * np.asarray(evk_a[j]).astype(object)) % mods
+    return moddown_ntt(acc0, qs, ps), moddown_ntt(acc1, qs, ps)
+
+
+# --------------------------------------------------------------------------------------
+# small-N key material for the decrypt check (not on the hot path)
+# --------------------------------------------------------------------------------------
+
+def _to_rns(poly, mods):
+    return np.stack([np.array([int(v) % m for v in poly], dtype=object) for m in mods])
+
+
+def gen_relin_key(s, qs, ps, dnum, rng):
+    """evk_j = (-a_j s + e_j + P g_j s^2, a_j) over Q u P, NTT form; g_j = CRT gadget of digit j
+    (g_j = 1 mod the primes of D_j, 0 mod the other primes of Q)."""
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    allm = qs + ps
+    n = len(s)
+    Q, P = math.prod(qs), math.prod(ps)
+    s_rns = _to_rns(s, allm)
+    s_n = rns_ntt_fwd(s_rns, allm)
+    mods = _mods_col(allm)
+    s2_n = s_n * s_n % mods
+    evk_b, evk_a = [], []
+    for lo, hi in digit_ranges(len(qs), dnum):
+        Dj = math.prod(qs[lo:hi])
+        Qhat = Q // Dj
+        g = Qhat * pow(Qhat % Dj, -1, Dj)
+        a = np.stack([np.array([rng.randrange(m) for _ in range(n)], dtype=object) for m in allm])
+        e = [rng.randrange(-3, 4) for _ in range(n)]
+        e_n = rns_ntt_fwd(_to_rns(e, allm), allm)
+        pg = np.array([(P * g) % m for m in allm], dtype=object).reshape(-1, 1)
+        b = (-a * s_n + e_n + pg * s2_n) % mods
+        evk_b.append(b)
+        evk_a.append(a)
+    return np.stack(evk_b), np.stack(evk_a)
+
+
+def crt_centered(x_rns, qs):
+    """CRT-reconstruct (L, N) residues to centred integers in (-Q/2, Q/2]."""
+    qs = [int(q) for q in qs]
+    Q = math.prod(qs)
+    acc = 0
+    for i, q in enumerate(qs):
+        hat = Q // q
+        acc = acc + np.asarray(x_rns[i]).astype(object) * (hat * pow(hat % q, -1, q))
+    acc = acc % Q
+    return np.where(acc > Q // 2, acc - Q, acc)
