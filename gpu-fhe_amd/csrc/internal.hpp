@@ -20,6 +20,8 @@ enum Status : int {
 };
 
 void set_error(const std::string& msg);
+// Records a timing mark after a launch when fhe_prof_begin() is active (prof.cpp).
+void prof_mark(hipStream_t s, const char* name);
 
 
 }  // namespace fhe

@@ -365,13 +365,17 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64* dst, u32 polys
   if (fwd) {
     k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(src, dst, nlimbs, limb0, pm, c->d_tw_fwd,
                                                  c->d_nfold, c->d_mods);
+    prof_mark(s, "ntt_col_fwd");
     k_ntt_row<LOGN, true><<<gr, G::THR_R, 0, s>>>(dst, dst, nlimbs, limb0, pm, c->d_tw_fwd,
                                                  c->d_mods);
+    prof_mark(s, "ntt_row_fwd");
   } else {
     k_ntt_row<LOGN, false><<<gr, G::THR_R, 0, s>>>(src, dst, nlimbs, limb0, pm, c->d_tw_inv,
                                                   c->d_mods);
+    prof_mark(s, "ntt_row_inv");
     k_ntt_col<LOGN, false><<<gc, G::THR_C, 0, s>>>(dst, dst, nlimbs, limb0, pm, c->d_tw_inv,
                                                   c->d_nfold, c->d_mods);
+    prof_mark(s, "ntt_col_inv");
   }
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;
@@ -389,14 +393,18 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   const dim3 gc((u32)((u64)batch * 2 * nlimbs * G::TILES_C));
   k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(a, x, nlimbs, limb0, to_x, c->d_tw_fwd,
                                                c->d_nfold, c->d_mods);
+  prof_mark(s, "hm_col_fwd_a");
   k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(b, x + 2 * limbN, nlimbs, limb0, to_x,
                                                c->d_tw_fwd, c->d_nfold, c->d_mods);
+  prof_mark(s, "hm_col_fwd_b");
   const dim3 gh((u32)((u64)batch * nlimbs * H::TILES));
   k_hommult_row<LOGN><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd, c->d_tw_inv,
                                             c->d_mods);
+  prof_mark(s, "hm_row_tensor");
   const dim3 gi((u32)((u64)batch * 3 * nlimbs * G::TILES_C));
   k_ntt_col<LOGN, false><<<gi, G::THR_C, 0, s>>>(d, d, nlimbs, limb0, flat_map(limbN),
                                                 c->d_tw_inv, c->d_nfold, c->d_mods);
+  prof_mark(s, "hm_col_inv");
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;
 }

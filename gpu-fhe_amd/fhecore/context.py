@@ -56,6 +56,8 @@ def to_device(x, device=None):
     if isinstance(x, torch.Tensor):
         return x.to(device or "cuda").contiguous()
     a = np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
+    if not a.flags.writeable:
+        a = a.copy()
     return torch.from_numpy(a.view(np.int64)).to(device or "cuda")
 
 

@@ -132,6 +132,14 @@ int fhe_keyswitch_shard(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const 
                         const uint64_t* d2_own, const uint64_t* evk_b, const uint64_t* evk_a,
                         uint32_t limb0, uint32_t nlimbs, void* workspace, fhe_stream_t stream);
 
+/* ---- timing marks (measurement support, not part of the reference surface) ------------------
+ * fhe_prof_begin records a HIP event on `stream`, then every kernel this host thread launches
+ * through libfhecore records one more event after itself (up to max_marks).  fhe_prof_end waits
+ * for the last event and returns the per-launch elapsed times (ms) and the kernel names,
+ * newline-separated, in launch order. */
+int fhe_prof_begin(uint32_t max_marks, fhe_stream_t stream);
+int fhe_prof_end(float* elapsed_ms, uint32_t cap, uint32_t* count, char* names, size_t names_cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,91 @@
+"""C-ABI boundary checks that need no GPU: the in-tree libfhecore loads, exports every symbol
+include/fhecore.h declares (and the ctypes table binds exactly those), host-only entry points
+agree with the oracle, and device entry points fail loudly -- never fall back -- without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import coracle
+from fhecore import _capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fhecore.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(fhe_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_reference_surface():
+    syms = declared_symbols()
+    for s in ("fhe_vec_add", "fhe_vec_sub", "fhe_vec_mul", "fhe_ntt_fwd", "fhe_ntt_inv",
+              "fhe_hommult", "fhe_baseconv", "fhe_keyswitch", "fhe_keyswitch_shard",
+              "fhe_ctx_create", "fhe_ctx_destroy", "fhe_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_capi.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(_capi.SIGNATURES) == declared_symbols()
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(_capi.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_gen_moduli_matches_oracle():
+    lib = _capi.load()
+    for log_n, count in [(12, 1), (14, 4), (16, 20), (17, 32)]:
+        out = (ctypes.c_uint64 * count)()
+        _capi.check(lib.fhe_gen_moduli(log_n, count, 60, 0, out), "gen")
+        assert [int(v) for v in out] == [int(v) for v in coracle.gen_moduli(log_n, count)]
+    out = (ctypes.c_uint64 * 4)()
+    _capi.check(lib.fhe_gen_moduli(16, 4, 60, 8, out), "gen skip")
+    assert [int(v) for v in out] == [int(v) for v in coracle.gen_moduli(16, 4, skip=8)]
+
+
+def test_errors_are_reported_not_raised():
+    lib = _capi.load()
+    rc = lib.fhe_gen_moduli(16, 1, 99, 0, (ctypes.c_uint64 * 1)())
+    assert rc == -1
+    assert b"bits" in lib.fhe_last_error()
+    with pytest.raises(_capi.FheError):
+        _capi.check(rc, "fhe_gen_moduli")
+    # null context / bad window on the device entry points: rejected before any HIP call
+    assert lib.fhe_ntt_fwd(None, None, 1, 0, 1, None) == -1
+    assert lib.fhe_vec_add(None, None, None, None, 1, 0, 1, None) == -1
+    assert lib.fhe_hommult_workspace(None, 1, 1) == 0
+
+
+def test_ctx_create_validates_moduli_before_touching_a_device():
+    lib = _capi.load()
+    ctx = ctypes.c_void_p()
+    bad = _capi.u64_array([97])  # not 1 mod 2N for N = 2^12
+    assert lib.fhe_ctx_create(ctypes.byref(ctx), 12, bad, 1, None, 0, 0, 0) == -1
+    assert b"not a prime" in lib.fhe_last_error()
+    assert lib.fhe_ctx_create(ctypes.byref(ctx), 9, bad, 1, None, 0, 0, 0) == -4
+
+
+def test_no_cpu_fallback_without_device():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    import fhecore
+
+    with pytest.raises(fhecore.FheError):
+        fhecore.Context(12, L=1)
+    import arithmetic
+
+    with pytest.raises(fhecore.FheError):
+        arithmetic.vec_add(np.zeros(4, np.uint64), np.zeros(4, np.uint64), 7)
+    with pytest.raises(fhecore.FheError):
+        arithmetic.NTT(np.zeros(4096, np.uint64))

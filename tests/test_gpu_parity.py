@@ -1,0 +1,281 @@
+"""GPU parity tests: libfhecore (hand-written gfx950 kernels, called through the C ABI via ctypes)
+against the exact CPU oracle and the reference-derived golden fixtures.  Bit-exact everywhere:
+all outputs are canonical residues.  Full BASELINE sizes are covered by direct oracle comparison
+(the C restatement finishes them in seconds) plus size-independent properties."""
+import os
+
+import numpy as np
+import pytest
+
+import coracle
+import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def fc():
+    import fhecore
+
+    return fhecore
+
+
+def rand(mods, log_n, lead=(), seed=0):
+    rng = np.random.default_rng(seed)
+    n = 1 << log_n
+    return np.stack([rng.integers(0, q, size=lead + (n,), dtype=np.uint64) for q in mods],
+                    axis=len(lead))
+
+
+_CTX = {}
+
+
+def ctx_for(fc, log_n, L, K=0, dnum=1):
+    key = (log_n, L, K, dnum)
+    if key not in _CTX:
+        _CTX[key] = fc.Context(log_n, L=L, K=K, dnum=dnum)
+    return _CTX[key]
+
+
+# ------------------------------------------------------------------------------------ NTT
+
+@pytest.mark.parametrize("log_n,L,polys", [(10, 3, 2), (11, 2, 1), (12, 1, 3), (13, 2, 1),
+                                           (14, 4, 2), (15, 2, 1), (16, 8, 2), (17, 4, 1)])
+def test_ntt_matches_oracle(fc, log_n, L, polys):
+    ctx = ctx_for(fc, log_n, L)
+    x = rand(ctx.moduli, log_n, (polys,), seed=log_n)
+    t = fc.to_device(x)
+    ctx.ntt_(t)
+    got = fc.to_host(t)
+    assert (got == coracle.ntt_fwd(x, ctx.moduli)).all()
+    ctx.intt_(t)
+    assert (fc.to_host(t) == x).all()
+
+
+def test_ntt_golden_naive_fixture(fc):
+    d = np.load(os.path.join(GOLDEN, "ntt_N4096_L1.npz"))
+    ctx = fc.Context(12, moduli=[int(q) for q in d["moduli"]])
+    assert ctx.psi[0] == int(d["psi"])
+    t = fc.to_device(d["x"])
+    ctx.ntt_(t)
+    assert (fc.to_host(t) == d["y"]).all()
+    ctx.intt_(t)
+    assert (fc.to_host(t) == d["x"]).all()
+
+
+def test_ntt_inverse_of_arbitrary_input(fc):
+    """iNTT is applied to data that was never a forward output (bit-reversed inputs)."""
+    ctx = ctx_for(fc, 14, 4)
+    y = rand(ctx.moduli, 14, (2,), seed=3)
+    t = fc.to_device(y)
+    ctx.intt_(t)
+    assert (fc.to_host(t) == coracle.ntt_inv(y, ctx.moduli)).all()
+
+
+def test_ntt_edge_values_and_limb_window(fc):
+    ctx = ctx_for(fc, 16, 8)
+    qs = ctx.moduli
+    n = 1 << 16
+    x = np.zeros((3, 4, n), dtype=np.uint64)
+    for li in range(4):
+        q = qs[2 + li]
+        x[0, li] = q - 1                       # all max
+        x[1, li, ::2] = q - 1                  # alternating
+        x[2, li, n - 1] = 1                    # single monomial X^(N-1)
+    t = fc.to_device(x)
+    ctx.ntt_(t, limb0=2)
+    got = fc.to_host(t)
+    assert (got == coracle.ntt_fwd(x, qs[2:6])).all()
+    ctx.intt_(t, limb0=2)
+    assert (fc.to_host(t) == x).all()
+
+
+def test_ntt_linearity_full_size(fc):
+    """NTT(a + b) = NTT(a) + NTT(b) at N = 2^17 (size-independent property)."""
+    ctx = ctx_for(fc, 17, 4)
+    a = fc.to_device(rand(ctx.moduli, 17, (1,), seed=1))
+    b = fc.to_device(rand(ctx.moduli, 17, (1,), seed=2))
+    s = ctx.vec("add", a, b)
+    ctx.ntt_(a)
+    ctx.ntt_(b)
+    ctx.ntt_(s)
+    assert (fc.to_host(ctx.vec("add", a, b)) == fc.to_host(s)).all()
+
+
+# ----------------------------------------------------------------------------- vec ops
+
+@pytest.mark.parametrize("op", ["add", "sub", "mul"])
+def test_vec_ctx_golden(fc, op):
+    d = np.load(os.path.join(GOLDEN, "vec_N16384_L4.npz"))
+    ctx = fc.Context(14, moduli=[int(q) for q in d["moduli"]])
+    out = ctx.vec(op, fc.to_device(d["a"]), fc.to_device(d["b"]))
+    assert (fc.to_host(out) == d[op]).all()
+
+
+@pytest.mark.parametrize("fx", ["vec_N4096_L1.npz", "vec_N16384_L4.npz"])
+@pytest.mark.parametrize("op", ["add", "sub", "mul"])
+def test_reference_shim_golden(fc, fx, op):
+    import arithmetic
+
+    d = np.load(os.path.join(GOLDEN, fx))
+    col = np.array([int(q) for q in d["moduli"]], dtype=np.uint64).reshape(-1, 1)
+    fn = getattr(arithmetic, "vec_" + op)
+    got = fn(d["a"], d["b"], col)
+    assert got.dtype == np.uint64 and (got == d[op]).all()
+    got_obj = fn(d["a"].astype(object), d["b"].astype(object), col.astype(object))
+    assert got_obj.dtype == object and (got_obj.astype(np.uint64) == d[op]).all()
+
+
+def test_reference_shim_generic_moduli(fc):
+    import arithmetic
+
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, 2**64 - 1, (3, 500), dtype=np.uint64, endpoint=True)
+    b = rng.integers(0, 2**64 - 1, (3, 500), dtype=np.uint64, endpoint=True)
+    for mod in [7, 2**31 - 1, 2**61 - 1, 2**63 + 29, 2**64 - 59,
+                np.array([[3], [2**40 + 15], [2**62 + 135]], dtype=object),
+                np.arange(2, 502, dtype=np.uint64)]:
+        for op in ("add", "sub", "mul"):
+            got = getattr(arithmetic, "vec_" + op)(a, b, mod)
+            want = getattr(pyoracle, "vec_" + op)(a, b, np.asarray(mod, dtype=object))
+            assert (got.astype(object) == want).all(), (op, mod)
+    # signed operands (Python floor-mod semantics)
+    x = rng.integers(-2**62, 2**62, (2, 64), dtype=np.int64)
+    y = rng.integers(-2**62, 2**62, (2, 64), dtype=np.int64)
+    for op in ("add", "sub", "mul"):
+        got = getattr(arithmetic, "vec_" + op)(x, y, 1000003)
+        want = getattr(pyoracle, "vec_" + op)(x, y, 1000003)
+        assert (got.astype(object) == want).all(), op
+    with pytest.raises(AssertionError):
+        arithmetic.vec_add(a, b[:, :10], 7)
+
+
+def test_reference_shim_ntt_and_poly_add(fc):
+    import arithmetic
+    import polynomial
+
+    d = np.load(os.path.join(GOLDEN, "ntt_N4096_L1.npz"))
+    y = arithmetic.NTT(d["x"])  # default modulus chain = the fixture's modulus
+    assert (y == d["y"]).all()
+    assert (arithmetic.iNTT(y) == d["x"]).all()
+    y1 = arithmetic.NTT(d["x"][0], MOD=int(d["moduli"][0]))
+    assert (y1 == d["y"][0]).all()
+    v = np.load(os.path.join(GOLDEN, "vec_N16384_L4.npz"))
+    col = v["moduli"].reshape(-1, 1)
+    r = polynomial.poly_add((v["a"], v["b"]), (v["b"], v["a"]), col)
+    assert isinstance(r, tuple) and (r[0] == v["add"]).all() and (r[1] == v["add"]).all()
+
+
+# ------------------------------------------------------------------------------- HomMult
+
+def test_hommult_config3_matches_oracle(fc):
+    ctx = ctx_for(fc, 16, 8)
+    a = rand(ctx.moduli, 16, (2, 2), seed=21)
+    b = rand(ctx.moduli, 16, (2, 2), seed=22)
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    assert (d == coracle.hommult(a, b, ctx.moduli)).all()
+
+
+def test_hommult_small_schoolbook(fc):
+    ctx = ctx_for(fc, 10, 2)
+    a = rand(ctx.moduli, 10, (2,), seed=4)
+    b = rand(ctx.moduli, 10, (2,), seed=5)
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    for li, q in enumerate(ctx.moduli):
+        assert (d[0, li].astype(object) == pyoracle.negacyclic_mul(a[0, li], b[0, li], q)).all()
+
+
+def test_hommult_identity_ciphertext(fc):
+    """b = (1, 0): d0 = a0, d1 = a1, d2 = 0 at N = 2^16 (property, no oracle)."""
+    ctx = ctx_for(fc, 16, 8)
+    a = rand(ctx.moduli, 16, (3, 2), seed=30)
+    b = np.zeros_like(a)
+    b[:, 0, :, 0] = 1
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    assert (d[:, 0] == a[:, 0]).all() and (d[:, 1] == a[:, 1]).all() and (d[:, 2] == 0).all()
+
+
+def test_hommult_limb_window(fc):
+    ctx = ctx_for(fc, 14, 4)
+    a = rand(ctx.moduli[1:3], 14, (1, 2), seed=40)
+    b = rand(ctx.moduli[1:3], 14, (1, 2), seed=41)
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b), limb0=1))
+    assert (d == coracle.hommult(a, b, ctx.moduli[1:3])).all()
+
+
+# ------------------------------------------------------------------ base conversion / key-switch
+
+def test_baseconv_matches_oracle(fc):
+    ctx = ctx_for(fc, 16, 16, K=4, dnum=4)
+    mods = ctx.all_moduli
+    x = rand(mods[2:6], 16, seed=50)
+    out = fc.to_host(ctx.baseconv(fc.to_device(x), 2, 10, 10))
+    assert (out == coracle.baseconv(x, mods[2:6], mods[10:20])).all()
+
+
+@pytest.mark.parametrize("L,K,dnum", [(16, 4, 4), (8, 2, 3)])
+def test_keyswitch_matches_oracle(fc, L, K, dnum):
+    ctx = ctx_for(fc, 16, L, K=K, dnum=dnum)
+    allm = ctx.all_moduli
+    d2 = rand(ctx.moduli, 16, seed=60)
+    eb = rand(allm, 16, (dnum,), seed=61)
+    ea = rand(allm, 16, (dnum,), seed=62)
+    ks0, ks1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(eb), fc.to_device(ea))
+    r0, r1 = coracle.keyswitch(d2, eb, ea, ctx.moduli, ctx.special, dnum)
+    assert (fc.to_host(ks0) == r0).all() and (fc.to_host(ks1) == r1).all()
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_keyswitch_sharded_equals_unsharded(fc, G):
+    """the G-way limb-sharded key-switch (one all-gather of INTT(d2)) concatenates to
+    the single-device result bit for bit.  G shards run one after another on this one GPU."""
+    L, K, dnum = 16, 4, 4
+    ctx = ctx_for(fc, 16, L, K=K, dnum=dnum)
+    d2 = rand(ctx.moduli, 16, seed=70)
+    eb = rand(ctx.all_moduli, 16, (dnum,), seed=71)
+    ea = rand(ctx.all_moduli, 16, (dnum,), seed=72)
+    full0, full1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(eb), fc.to_device(ea))
+    c_all = fc.to_device(d2)
+    ctx.intt_(c_all)
+    nl = L // G
+    parts0, parts1 = [], []
+    for r in range(G):
+        lo = r * nl
+        own = np.concatenate([np.arange(lo, lo + nl), np.arange(L, L + K)])
+        k0, k1 = ctx.keyswitch_shard(c_all, fc.to_device(d2[lo:lo + nl]),
+                                     fc.to_device(np.ascontiguousarray(eb[:, own])),
+                                     fc.to_device(np.ascontiguousarray(ea[:, own])), lo)
+        parts0.append(fc.to_host(k0))
+        parts1.append(fc.to_host(k1))
+    assert (np.concatenate(parts0) == fc.to_host(full0)).all()
+    assert (np.concatenate(parts1) == fc.to_host(full1)).all()
+
+
+def test_keyswitch_decrypts_with_real_keys_on_gpu(fc):
+    import random
+
+    log_n, L, K, dnum = 10, 4, 2, 2
+    n = 1 << log_n
+    ctx = fc.Context(log_n, L=L, K=K, dnum=dnum)
+    qs, ps = ctx.moduli, ctx.special
+    rng = random.Random(5)
+    s = [rng.randrange(-1, 2) for _ in range(n)]
+    evk_b, evk_a = pyoracle.gen_relin_key(s, qs, ps, dnum, rng)
+    d2 = np.stack([np.array([rng.randrange(q) for _ in range(n)], dtype=np.uint64) for q in qs])
+    ks0, ks1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(evk_b.astype(np.uint64)),
+                             fc.to_device(evk_a.astype(np.uint64)))
+    ks0, ks1 = fc.to_host(ks0).astype(object), fc.to_host(ks1).astype(object)
+    col = pyoracle._mods_col(qs)
+    sn = pyoracle.rns_ntt_fwd(pyoracle._to_rns(s, qs), qs)
+    err = (ks0 + ks1 * sn - d2.astype(object) * sn * sn) % col
+    e = pyoracle.crt_centered(pyoracle.rns_ntt_inv(err, qs), qs)
+    assert max(abs(int(v)) for v in e) < 1 << 20
+
+
+def test_bad_window_is_rejected(fc):
+    ctx = ctx_for(fc, 12, 1)
+    t = fc.to_device(np.zeros((1, 2, 4096), np.uint64))
+    with pytest.raises(fc.FheError):
+        ctx.ntt_(t)  # 2 limbs on a 1-limb context
