@@ -27,8 +27,26 @@
 namespace fhe {
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kElog = 4;  // 16 elements per thread per round
+// FHE_ELOG: log2 of the elements a thread holds per round (16 -> rounds of up to 4 stages;
+// 8 -> rounds of up to 3 stages, half the LDS and VGPRs per wave, twice the waves per CU).
+#ifndef FHE_ELOG
+#define FHE_ELOG 4
+#endif
+constexpr int kElog = FHE_ELOG;
+constexpr int kE = 1 << kElog;
+constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per workgroup
+// FHE_NTT_ABLATE (timing-only A/B builds, tools/build_variant.sh; never the shipped library):
+// 1 = skip the butterflies of the generic passes, 2 = skip their global loads/stores.
+#ifndef FHE_NTT_ABLATE
+#define FHE_NTT_ABLATE 0
+#endif
+// FHE_BFLY_ASM: butterflies through the inline-asm helpers of modarith.hpp (1) or plain C++ (0).
+#ifndef FHE_BFLY_ASM
+#define FHE_BFLY_ASM 0
+#endif
+#ifndef FHE_NTT_MIN_WAVES
+#define FHE_NTT_MIN_WAVES 1
+#endif
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -49,11 +67,9 @@ struct Rounds {
     for (int i = 0; i < k; ++i) hi -= kb(i);
     return hi - kb(k);
   }
-  static constexpr int lo_inv(int k) {
-    int lo = 0;
-    for (int i = 0; i < k; ++i) lo += kb(i);
-    return lo;
-  }
+  // the inverse runs the forward's rounds in mirror order (bottom bits first)
+  static constexpr int kb_inv(int k) { return kb(NR - 1 - k); }
+  static constexpr int lo_inv(int k) { return lo_fwd(NR - 1 - k); }
 };
 
 // Which position bits of the sub-transform a thread's element index j owns in one round:
@@ -61,7 +77,7 @@ struct Rounds {
 // positions; the thread index fills every other bit, ascending.
 template <int LOGR, int KB, int LO>
 struct Layout {
-  static constexpr int E = 1 << kElog;
+  static constexpr int E = kE;
   static constexpr int ex_pos(int k) {
     int found = 0;
     for (int i = 0; i < LOGR; ++i) {
@@ -95,6 +111,22 @@ struct Layout {
 
 enum Final : int { kNotFinal = 0, kFinalFwd = 1, kFinalInv = 2 };
 
+// LDS exchange fences.  A row sub-transform's threads all sit in one wavefront, so the row
+// kernels only need wavefront-scope ordering of their LDS traffic (DS instructions of one wave
+// execute in issue order): no s_barrier, and waves drift apart freely, overlapping one wave's
+// global loads with another's butterflies.  The column pass spans waves and uses the block barrier.
+enum Sync : int { kBlockSync = 0, kWaveSync = 1 };
+template <int S>
+__device__ __forceinline__ void lds_sync() {
+  if constexpr (S == kBlockSync) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // Maps a launch's poly index p to element offsets: p = g * pg + k reads src + g*sgs + k*sps and
 // writes dst + g*dgs + k*dps (lets HomMult scatter a/b into its 4-slot workspace).
 struct PolyMap {
@@ -105,22 +137,18 @@ struct PolyMap {
 };
 static inline PolyMap flat_map(u64 pstride) { return PolyMap{1, pstride, 0, pstride, 0}; }
 
-// One round: load 16 elements of this thread's sub-transform from LDS (element at position p
-// lives at s[p * ps]), run the round's stages, store back.  `base` selects the twiddle rows:
-// local stage st, group g reads tw[(base << st) + g] (base = 1 for the column pass,
-// R1 + row for the row pass).
+// Runs one round's butterfly stages on the 16 values a thread holds in registers.
+// Element j sits at sub-transform position tp | Lay::jpos(j).  `base` selects the twiddle rows:
+// local stage st, group g reads tw[(base << st) + g] (base = 1 for the column pass, R1 + row for
+// the row pass).
 template <int LOGR, int KB, int LO, bool FWD, int FIN>
-__device__ __forceinline__ void ntt_round(u64* __restrict__ s, const int ps, const u32 t,
-                                          const ulonglong2* __restrict__ tw, const u32 base,
-                                          const u64 q, const ulonglong2 nf0, const ulonglong2 nf1) {
+__device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
+                                              const ulonglong2* __restrict__ tw, const u32 base,
+                                              const u64 q, const ulonglong2 nf0,
+                                              const ulonglong2 nf1) {
   using Lay = Layout<LOGR, KB, LO>;
   constexpr int E = Lay::E;
-  const u32 tp = Lay::tpos(t);
-  const u64 q2 = 2 * q;
-  u64 x[E];
-#pragma unroll
-  for (int j = 0; j < E; ++j) x[j] = s[(tp | Lay::jpos(j)) * ps];
-
+  const u64 q2 = 2 * q, nq = 0 - q, nq2 = 0 - q2, q2p1 = q2 + 1;
   if constexpr (FWD) {
 #pragma unroll
     for (int b = KB - 1; b >= 0; --b) {
@@ -132,10 +160,18 @@ __device__ __forceinline__ void ntt_round(u64* __restrict__ s, const int ps, con
         const int jj = j | (1 << b);
         const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(j) >> (bitpos + 1));
         const ulonglong2 w = tw[(base << st) + g];
+        // Harvey CT: u in [0, 4q) -> [0, 2q); v = w x[jj] in [0, 2q); outputs in [0, 4q)
+#if FHE_BFLY_ASM
+        const u64 u = csub_fast(x[j], nq2);
+        const u64 v = shoup_fast(x[jj], w.x, w.y, nq);
+        x[j] = add64(u, v);
+        x[jj] = sub_plus(u, v, q2p1);
+#else
         const u64 u = csub(x[j], q2);
         const u64 v = shoup_lazy(x[jj], w.x, w.y, q);
         x[j] = u + v;
         x[jj] = u - v + q2;
+#endif
       }
     }
     if constexpr (FIN == kFinalFwd) {
@@ -151,8 +187,13 @@ __device__ __forceinline__ void ntt_round(u64* __restrict__ s, const int ps, con
       for (int j = 0; j < E; ++j) {
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
+        // Harvey GS: inputs in [0, 2q); sum -> [0, 2q); (u - v + 2q) w -> [0, 2q)
         const u64 u = x[j], v = x[jj];
+#if FHE_BFLY_ASM
+        const u64 sum = add64(u, v), dif = sub_plus(u, v, q2p1);
+#else
         const u64 sum = u + v, dif = u - v + q2;
+#endif
         if (FIN == kFinalInv && st == 0) {
           // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
           x[j] = csub(shoup_lazy(sum, nf0.x, nf0.y, q), q);
@@ -160,29 +201,123 @@ __device__ __forceinline__ void ntt_round(u64* __restrict__ s, const int ps, con
         } else {
           const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(j) >> (bitpos + 1));
           const ulonglong2 w = tw[(base << st) + g];
+#if FHE_BFLY_ASM
+          x[j] = csub_fast(sum, nq2);
+          x[jj] = shoup_fast(dif, w.x, w.y, nq);
+#else
           x[j] = csub(sum, q2);
           x[jj] = shoup_lazy(dif, w.x, w.y, q);
+#endif
         }
       }
     }
   }
-#pragma unroll
-  for (int j = 0; j < E; ++j) s[(tp | Lay::jpos(j)) * ps] = x[j];
 }
 
-// All rounds of a 2^LOGR-point sub-transform held in LDS. Caller syncs before and after.
-template <int LOGR, bool FWD, int FIN>
-__device__ __forceinline__ void ntt_sub(u64* s, int ps, u32 t, bool active,
-                                        const ulonglong2* __restrict__ tw, u32 base, u64 q,
-                                        ulonglong2 nf0, ulonglong2 nf1) {
+// Whether a round's kE positions are tp + 0..kE-1 (contiguous words: 16-byte accesses).
+template <class Lay>
+constexpr bool contiguous16() {
+  for (int j = 0; j < kE; ++j)
+    if (Lay::jpos(j) != (u32)j) return false;
+  return true;
+}
+
+// Global-memory views of one sub-transform.  Column pass: position p at base[p * R2] (lanes run
+// over adjacent columns, so every access is coalesced).  Row pass: position p at base[p].
+template <int STRIDE>
+struct GView {
+  u64* base;
+  template <class Lay>
+  __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
+    if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
+      const ulonglong2* v = reinterpret_cast<const ulonglong2*>(base + tp);
+#pragma unroll
+      for (int j = 0; j < kE / 2; ++j) {
+        const ulonglong2 w = v[j];
+        x[2 * j] = w.x;
+        x[2 * j + 1] = w.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kE; ++j) x[j] = base[(u64)(tp | Lay::jpos(j)) * STRIDE];
+    }
+  }
+  template <class Lay>
+  __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
+    if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
+      ulonglong2* v = reinterpret_cast<ulonglong2*>(base + tp);
+#pragma unroll
+      for (int j = 0; j < kE / 2; ++j) v[j] = make_ulonglong2(x[2 * j], x[2 * j + 1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kE; ++j) base[(u64)(tp | Lay::jpos(j)) * STRIDE] = x[j];
+    }
+  }
+};
+
+// LDS view of one sub-transform: position p at s[p * PS + (PAD16 ? p >> 4 : 0)].
+template <int PS, bool PAD16>
+struct LView {
+  u64* s;
+  __device__ __forceinline__ u32 idx(u32 p) const { return p * PS + (PAD16 ? (p >> 4) : 0); }
+  template <class Lay>
+  __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
+#pragma unroll
+    for (int j = 0; j < kE; ++j) x[j] = s[idx(tp | Lay::jpos(j))];
+  }
+  template <class Lay>
+  __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
+#pragma unroll
+    for (int j = 0; j < kE; ++j) s[idx(tp | Lay::jpos(j))] = x[j];
+  }
+};
+
+// A whole 2^LOGR-point pass for one sub-transform: round 0 loads straight from global memory,
+// rounds exchange through LDS, the last round stores straight to global memory.  Every thread
+// of the workgroup must call this (it contains barriers); `active` masks the arithmetic/IO.
+template <int LOGR, bool FWD, int FIN, int SYNC, class GIn, class GOut, class LV>
+__device__ __forceinline__ void ntt_pass(const GIn& gin, const GOut& gout, const LV& lv, u32 t,
+                                         bool active, const ulonglong2* __restrict__ tw, u32 base,
+                                         u64 q, ulonglong2 nf0, ulonglong2 nf1) {
   using Rd = Rounds<LOGR>;
+  u64 x[kE];
   static_for<0, Rd::NR>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
-    constexpr int KB = Rd::kb(k);
+    constexpr int KB = FWD ? Rd::kb(k) : Rd::kb_inv(k);
     constexpr int LO = FWD ? Rd::lo_fwd(k) : Rd::lo_inv(k);
     constexpr int F = (k == Rd::NR - 1) ? FIN : kNotFinal;
-    if (k > 0) __syncthreads();
-    if (active) ntt_round<LOGR, KB, LO, FWD, F>(s, ps, t, tw, base, q, nf0, nf1);
+    using Lay = Layout<LOGR, KB, LO>;
+    const u32 tp = Lay::tpos(t);
+    if constexpr (k == 0) {
+#if FHE_NTT_ABLATE == 2  // timing-only build: no global loads (synthetic values)
+      if (active)
+        for (int j = 0; j < kE; ++j) x[j] = (u64)(tp + j) * 0x9e3779b97f4a7c15ull % q;
+#else
+      if (active) gin.template load<Lay>(x, tp);
+#endif
+    } else {
+      lds_sync<SYNC>();
+      if (active) lv.template load<Lay>(x, tp);
+    }
+#if FHE_NTT_ABLATE == 1  // timing-only build: no butterflies
+    for (int j = 0; j < kE; ++j) asm volatile("" : "+v"(x[j]));
+#else
+    if (active) round_compute<LOGR, KB, LO, FWD, F>(x, tp, tw, base, q, nf0, nf1);
+#endif
+    if constexpr (k == Rd::NR - 1) {
+#if FHE_NTT_ABLATE == 2
+      if (active) {
+        u64 acc = 0;
+        for (int j = 0; j < kE; ++j) acc ^= x[j];
+        if (acc == 0x5a5a5a5a5a5a5a5aull) gout.template store<Lay>(x, tp);  // practically never
+      }
+#else
+      if (active) gout.template store<Lay>(x, tp);
+#endif
+    } else {
+      if (k > 0) lds_sync<SYNC>();
+      if (active) lv.template store<Lay>(x, tp);
+    }
   });
 }
 
@@ -190,24 +325,24 @@ template <int LOGN>
 struct Geo {
   static constexpr int N1 = LOGN / 2, N2 = LOGN - N1;
   static constexpr int R1 = 1 << N1, R2 = 1 << N2;  // R1 rows x R2 columns
-  // column pass: SUBS_C columns per workgroup
+  // column pass: SUBS_C columns per workgroup, lanes run over columns
   static constexpr int TPS_C = R1 >> kElog;
   static constexpr int SUBS_C = (kThreads / TPS_C) < R2 ? (kThreads / TPS_C) : R2;
   static constexpr int THR_C = SUBS_C * TPS_C;
-  static constexpr int PAD_C = 1;
-  static constexpr int LDS_C = R1 * (SUBS_C + PAD_C);
+  static constexpr int CS = SUBS_C + 1;  // LDS row stride (words)
+  static constexpr int LDS_C = R1 * CS;
   static constexpr int TILES_C = R2 / SUBS_C;
-  // row pass: SUBS_R rows per workgroup
+  // row pass: SUBS_R rows per workgroup, lanes run along a row
   static constexpr int TPS_R = R2 >> kElog;
   static constexpr int SUBS_R = (kThreads / TPS_R) < R1 ? (kThreads / TPS_R) : R1;
   static constexpr int THR_R = SUBS_R * TPS_R;
-  static constexpr int PAD_R = 1;
-  static constexpr int LDS_R = SUBS_R * (R2 + PAD_R);
+  static constexpr int RS = R2 + R2 / 16;  // LDS row stride (one pad word per 16)
+  static constexpr int LDS_R = SUBS_R * RS;
   static constexpr int TILES_R = R1 / SUBS_R;
   static_assert(N1 >= kElog - 1 && N2 >= kElog, "log N too small for this kernel family");
 };
 
-// Column pass. src/dst: [polys][nlimbs][N] with poly stride pstride; grid = polys*nlimbs*TILES_C.
+// Column pass. src/dst: [polys][nlimbs][N] via PolyMap; grid = polys * nlimbs * TILES_C.
 template <int LOGN, bool FWD>
 __global__ __launch_bounds__(kThreads) void k_ntt_col(const u64* __restrict__ src,
                                                       u64* __restrict__ dst, u32 nlimbs,
@@ -223,33 +358,22 @@ __global__ __launch_bounds__(kThreads) void k_ntt_col(const u64* __restrict__ sr
   const u32 l = pl % nlimbs, p = pl / nlimbs;
   const u32 limb = limb0 + l;
   const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
-  const u64* sp = src + pm.src(p) + loc;
-  u64* dp = dst + pm.dst(p) + loc;
   const u64 q = mods[limb].q;
   const ulonglong2* tw = tw_all + (u64)limb * N;
-  const u32 tid = threadIdx.x;
-
-  for (u32 e = tid; e < (u32)(G::R1 * G::SUBS_C); e += G::THR_C) {
-    const u32 row = e / G::SUBS_C, col = e % G::SUBS_C;
-    lds[row * (G::SUBS_C + G::PAD_C) + col] = sp[(u64)row * G::R2 + col];
-  }
-  __syncthreads();
-  const u32 sub = tid % G::SUBS_C, t = tid / G::SUBS_C;
+  const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
   ulonglong2 nf0 = {0, 0}, nf1 = {0, 0};
   if (!FWD) {
     nf0 = nfold[2 * limb];
     nf1 = nfold[2 * limb + 1];
   }
-  ntt_sub<G::N1, FWD, FWD ? kNotFinal : kFinalInv>(lds + sub, G::SUBS_C + G::PAD_C, t, true, tw,
-                                                   1u, q, nf0, nf1);
-  __syncthreads();
-  for (u32 e = tid; e < (u32)(G::R1 * G::SUBS_C); e += G::THR_C) {
-    const u32 row = e / G::SUBS_C, col = e % G::SUBS_C;
-    dp[(u64)row * G::R2 + col] = lds[row * (G::SUBS_C + G::PAD_C) + col];
-  }
+  const GView<G::R2> gin{const_cast<u64*>(src) + pm.src(p) + loc + sub};
+  const GView<G::R2> gout{dst + pm.dst(p) + loc + sub};
+  const LView<G::CS, false> lv{lds + sub};
+  ntt_pass<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync>(gin, gout, lv, t, true, tw, 1u, q,
+                                                               nf0, nf1);
 }
 
-// Row pass. grid = polys*nlimbs*TILES_R.
+// Row pass. grid = polys * nlimbs * TILES_R.
 template <int LOGN, bool FWD>
 __global__ __launch_bounds__(kThreads) void k_ntt_row(const u64* __restrict__ src,
                                                       u64* __restrict__ dst, u32 nlimbs,
@@ -263,36 +387,35 @@ __global__ __launch_bounds__(kThreads) void k_ntt_row(const u64* __restrict__ sr
   const u32 pl = blockIdx.x / G::TILES_R;
   const u32 l = pl % nlimbs, p = pl / nlimbs;
   const u32 limb = limb0 + l;
-  const u64 loc = (u64)l * N + (u64)tile * G::SUBS_R * G::R2;
-  const u64* sp = src + pm.src(p) + loc;
-  u64* dp = dst + pm.dst(p) + loc;
+  const u32 t = threadIdx.x % G::TPS_R, sub = threadIdx.x / G::TPS_R;
+  const u32 row = tile * G::SUBS_R + sub;
+  const u64 loc = (u64)l * N + (u64)row * G::R2;
   const u64 q = mods[limb].q;
   const ulonglong2* tw = tw_all + (u64)limb * N;
-  const u32 tid = threadIdx.x;
-
-  for (u32 e = tid; e < (u32)(G::SUBS_R * G::R2); e += G::THR_R)
-    lds[(e / G::R2) * (G::R2 + G::PAD_R) + e % G::R2] = sp[e];
-  __syncthreads();
-  const u32 sub = tid % G::SUBS_R, t = tid / G::SUBS_R;
-  const u32 row = tile * G::SUBS_R + sub;
-  ntt_sub<G::N2, FWD, FWD ? kFinalFwd : kNotFinal>(lds + sub * (G::R2 + G::PAD_R), 1, t, true,
-                                                   tw, (u32)G::R1 + row, q, {0, 0}, {0, 0});
-  __syncthreads();
-  for (u32 e = tid; e < (u32)(G::SUBS_R * G::R2); e += G::THR_R)
-    dp[e] = lds[(e / G::R2) * (G::R2 + G::PAD_R) + e % G::R2];
+  const GView<1> gin{const_cast<u64*>(src) + pm.src(p) + loc};
+  const GView<1> gout{dst + pm.dst(p) + loc};
+  const LView<1, true> lv{lds + sub * G::RS};
+  static_assert(64 % G::TPS_R == 0, "a row must not straddle wavefronts");
+  ntt_pass<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync>(gin, gout, lv, t, true, tw,
+                                                               (u32)G::R1 + row, q, {0, 0}, {0, 0});
 }
 
 // Fused HomMult row kernel: rows of the 4 column-transformed inputs (layout [batch][4][nlimbs][N]
 // in `x`: A0, A1, B0, B1) -> row-forward, tensor, row-inverse -> d [batch][3][nlimbs][N].
+// Thread groups g = 0..3 own one polynomial each; after the forward rows every group writes its
+// canonical values to LDS slot g, groups 0..2 then form d_g from the slots at the same positions
+// and run the inverse rows (group 3 idles through them).
 template <int LOGN>
 struct HmGeo {
   using G = Geo<LOGN>;
   static constexpr int TPS = G::TPS_R;
-  static constexpr int ROWS = (kThreads / 4 / TPS) < 1 ? 1 : (kThreads / 4 / TPS);
-  static constexpr int THR = 4 * ROWS * TPS;
-  static constexpr int STRIDE = G::R2 + 1;
-  static constexpr int SLOT = ROWS * STRIDE;
+  static constexpr int LANES_ROW = 4 * TPS;                  // 4 polys x TPS threads per row
+  static constexpr int ROWS = kThreads / LANES_ROW;          // rows per workgroup
+  static constexpr int THR = ROWS * LANES_ROW;
+  static constexpr int ROWW = 4 * G::RS;                     // LDS words per row (4 slots)
   static constexpr int TILES = G::R1 / ROWS;
+  static_assert(64 % LANES_ROW == 0 || LANES_ROW % 64 == 0, "row group vs wavefront");
+  static constexpr int SYNC = LANES_ROW <= 64 ? kWaveSync : kBlockSync;
 };
 
 template <int LOGN>
@@ -304,8 +427,9 @@ __global__ __launch_bounds__(kThreads) void k_hommult_row(const u64* __restrict_
                                                           const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
   using H = HmGeo<LOGN>;
+  using Rd = Rounds<G::N2>;
   constexpr u64 N = 1ull << LOGN;
-  __shared__ u64 lds[4 * H::SLOT];
+  __shared__ u64 lds[H::ROWS * H::ROWW];
   const u32 tile = blockIdx.x % H::TILES;
   const u32 bl = blockIdx.x / H::TILES;
   const u32 l = bl % nlimbs, b = bl / nlimbs;
@@ -313,47 +437,81 @@ __global__ __launch_bounds__(kThreads) void k_hommult_row(const u64* __restrict_
   const ModParams m = mods[limb];
   const u64 q = m.q;
   const u64 limbN = (u64)nlimbs * N;
-  const u64 rowoff = (u64)l * N + (u64)tile * H::ROWS * G::R2;
-  const u32 tid = threadIdx.x;
-  constexpr u32 TILE_ELEMS = H::ROWS * G::R2;
-
-  // load 4 polys
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const u64* src = x + ((u64)b * 4 + k) * limbN + rowoff;
-    for (u32 e = tid; e < TILE_ELEMS; e += H::THR)
-      lds[k * H::SLOT + (e / G::R2) * H::STRIDE + e % G::R2] = src[e];
-  }
-  __syncthreads();
-  const u32 poly = tid / (H::ROWS * H::TPS);
-  const u32 rem = tid % (H::ROWS * H::TPS);
-  const u32 sub = rem % H::ROWS, t = rem / H::ROWS;
+  const u32 sub = threadIdx.x / H::LANES_ROW;
+  const u32 rem = threadIdx.x % H::LANES_ROW;
+  const u32 grp = rem / H::TPS, t = rem % H::TPS;
   const u32 row = tile * H::ROWS + sub;
-  u64* my = lds + poly * H::SLOT + sub * H::STRIDE;
-  ntt_sub<G::N2, true, kFinalFwd>(my, 1, t, true, twf + (u64)limb * N, (u32)G::R1 + row, q,
-                                  {0, 0}, {0, 0});
-  __syncthreads();
-  // tensor in place: slots 0,1,2 <- d0, d1, d2
-  for (u32 e = tid; e < TILE_ELEMS; e += H::THR) {
-    const u32 li = (e / G::R2) * H::STRIDE + e % G::R2;
-    const u64 a0 = lds[li], a1 = lds[H::SLOT + li];
-    const u64 b0 = lds[2 * H::SLOT + li], b1 = lds[3 * H::SLOT + li];
-    lds[li] = mulmod_barrett(a0, b0, m);
-    lds[H::SLOT + li] = barrett_reduce((u128)a0 * b1 + (u128)a1 * b0, m);
-    lds[2 * H::SLOT + li] = mulmod_barrett(a1, b1, m);
-  }
-  __syncthreads();
-  ntt_sub<G::N2, false, kNotFinal>(my, 1, t, poly < 3, twi + (u64)limb * N, (u32)G::R1 + row, q,
-                                   {0, 0}, {0, 0});
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    u64* out = d + ((u64)b * 3 + k) * limbN + rowoff;
-    for (u32 e = tid; e < TILE_ELEMS; e += H::THR)
-      out[e] = lds[k * H::SLOT + (e / G::R2) * H::STRIDE + e % G::R2];
-  }
-}
+  const u64 loc = (u64)l * N + (u64)row * G::R2;
+  const ulonglong2* tf = twf + (u64)limb * N;
+  const ulonglong2* ti = twi + (u64)limb * N;
+  const u32 base = (u32)G::R1 + row;
+  u64* rowlds = lds + sub * H::ROWW;
+  const LView<1, true> own{rowlds + grp * G::RS};
+  constexpr int SY = H::SYNC;
 
+  // forward row pass: round 0 from global, rounds exchange through LDS, last round stays in VGPRs
+  u64 v[kE];
+  static_for<0, Rd::NR>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int KB = Rd::kb(k);
+    constexpr int LO = Rd::lo_fwd(k);
+    constexpr int F = (k == Rd::NR - 1) ? kFinalFwd : kNotFinal;
+    using Lay = Layout<G::N2, KB, LO>;
+    const u32 tp = Lay::tpos(t);
+    if constexpr (k == 0) {
+      const GView<1> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc};
+      gin.template load<Lay>(v, tp);
+    } else {
+      lds_sync<SY>();
+      own.template load<Lay>(v, tp);
+    }
+    round_compute<G::N2, KB, LO, true, F>(v, tp, tf, base, q, {0, 0}, {0, 0});
+    if constexpr (k < Rd::NR - 1) {
+      if (k > 0) lds_sync<SY>();
+      own.template store<Lay>(v, tp);
+    }
+  });
+  // tensor: publish canonical A0, A1, B0, B1 at the last forward layout, combine per position
+  using LayT = Layout<G::N2, Rd::kb(Rd::NR - 1), Rd::lo_fwd(Rd::NR - 1)>;
+  const u32 tpT = LayT::tpos(t);
+  lds_sync<SY>();
+  own.template store<LayT>(v, tpT);
+  lds_sync<SY>();
+  const bool active = grp < 3;
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < kE; ++j) {
+      const u32 idx = own.idx(tpT | LayT::jpos(j));
+      const u64 a0 = rowlds[idx], a1 = rowlds[G::RS + idx];
+      const u64 b0 = rowlds[2 * G::RS + idx], b1 = rowlds[3 * G::RS + idx];
+      if (grp == 0) v[j] = mulmod_barrett(a0, b0, m);
+      else if (grp == 1) v[j] = barrett_reduce((u128)a0 * b1 + (u128)a1 * b0, m);
+      else v[j] = mulmod_barrett(a1, b1, m);
+    }
+  }
+  // inverse row pass: its first round butterflies the low bits, the layout the tensor used
+  static_assert(Rd::lo_fwd(Rd::NR - 1) == Rd::lo_inv(0) && Rd::kb(Rd::NR - 1) == Rd::kb_inv(0),
+                "tensor layout must match the first inverse round");
+  static_for<0, Rd::NR>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int KB = Rd::kb_inv(k);
+    constexpr int LO = Rd::lo_inv(k);
+    using Lay = Layout<G::N2, KB, LO>;
+    const u32 tp = Lay::tpos(t);
+    if constexpr (k > 0) {
+      lds_sync<SY>();
+      if (active) own.template load<Lay>(v, tp);
+    }
+    if (active) round_compute<G::N2, KB, LO, false, kNotFinal>(v, tp, ti, base, q, {0, 0}, {0, 0});
+    if constexpr (k == Rd::NR - 1) {
+      const GView<1> gout{d + ((u64)b * 3 + grp) * limbN + loc};
+      if (active) gout.template store<Lay>(v, tp);
+    } else {
+      lds_sync<SY>();
+      if (active) own.template store<Lay>(v, tp);
+    }
+  });
+}
 
 template <int LOGN>
 int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64* dst, u32 polys, u64 pstride,

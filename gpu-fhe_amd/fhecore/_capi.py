@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libfhecore.so")
+# FHECORE_LIB overrides the in-tree library (A/B builds of the same sources in tools/).
+LIB_PATH = os.environ.get("FHECORE_LIB") or os.path.join(_PKG_ROOT, "lib", "libfhecore.so")
 
 FHE_OK = 0
 _ERRNAMES = {-1: "FHE_EINVAL", -2: "FHE_ENOMEM", -3: "FHE_EDEVICE", -4: "FHE_EUNSUPPORTED"}
