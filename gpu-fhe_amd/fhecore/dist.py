@@ -1,0 +1,88 @@
+"""RNS-limb sharding across GPUs: one process per GPU, torch.distributed over RCCL.
+
+Every coefficient-wise op, NTT/INTT and the HomMult tensor is independent per RNS limb, so rank r
+of G simply owns a contiguous block of Q-limbs and runs those -- no collective.  The hybrid
+key-switch has exactly one exchange: each rank INTTs its own limbs of d2, one all-gather makes the
+full coefficient-form d2 available everywhere (ModUp needs every limb of a digit), and each rank
+then finishes ModUp / NTT / inner product / ModDown for its own Q-limbs plus a replicated copy of
+the K special limbs (so ModDown needs no second collective).  Outputs stay limb-sharded and
+concatenate to the single-device result bit for bit.
+
+The orchestration is written against an "engine" with two methods -- ``intt_(t, limb0)`` and
+``keyswitch_shard(c_all, d2_own, evk_b, evk_a, limb0)`` -- so fhecore.Context (the HIP path) and a
+CPU restatement used by the gloo tests run the same code.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass(frozen=True)
+class LimbShard:
+    """Rank `rank` of `world` owns Q-limbs [lo, hi) of an L-limb modulus chain."""
+
+    L: int
+    world: int
+    rank: int
+
+    def __post_init__(self):
+        if self.world < 1 or not 0 <= self.rank < self.world:
+            raise ValueError("bad rank/world")
+        if self.L % self.world:
+            raise ValueError(f"L = {self.L} limbs do not divide evenly over {self.world} ranks")
+
+    @property
+    def nlimbs(self) -> int:
+        return self.L // self.world
+
+    @property
+    def lo(self) -> int:
+        return self.rank * self.nlimbs
+
+    @property
+    def hi(self) -> int:
+        return self.lo + self.nlimbs
+
+    def own(self, x, limb_dim: int = -2):
+        """This rank's slice of a full-limb tensor/array along `limb_dim`."""
+        idx = [slice(None)] * x.dim() if hasattr(x, "dim") else [slice(None)] * x.ndim
+        idx[limb_dim] = slice(self.lo, self.hi)
+        return x[tuple(idx)]
+
+    def evk_rows(self, K: int):
+        """Row indices of an evk [dnum, L + K, N] this rank keeps: its Q-limbs, then all P-limbs."""
+        return list(range(self.lo, self.hi)) + list(range(self.L, self.L + K))
+
+    @classmethod
+    def from_env(cls, L: int, group=None):
+        if dist.is_available() and dist.is_initialized():
+            return cls(L, dist.get_world_size(group), dist.get_rank(group))
+        return cls(L, 1, 0)
+
+
+def all_gather_limbs(x_own, shard: LimbShard, group=None):
+    """[nlimbs, N] per rank -> [L, N] on every rank (rank order = limb order)."""
+    if shard.world == 1:
+        return x_own.contiguous()
+    out = torch.empty((shard.L,) + tuple(x_own.shape[1:]), dtype=x_own.dtype, device=x_own.device)
+    dist.all_gather_into_tensor(out, x_own.contiguous(), group=group)
+    return out
+
+
+def sharded_hommult(engine, a_own, b_own, shard: LimbShard, out=None, workspace=None):
+    """ct x ct tensor on this rank's limbs: a_own/b_own [batch, 2, nlimbs, N]. No collective."""
+    return engine.hommult(a_own, b_own, out=out, limb0=shard.lo, workspace=workspace)
+
+
+def sharded_keyswitch(engine, d2_own, evk_b_own, evk_a_own, shard: LimbShard, group=None):
+    """Hybrid key-switch of this rank's limbs (SURVEY.md §8a', §8e).
+
+    d2_own: [nlimbs, N] NTT form (limbs [lo, hi)); evk_*_own: [dnum, nlimbs + K, N] (own Q-limbs then
+    the K P-limbs, see LimbShard.evk_rows).  Returns (ks0_own, ks1_own), [nlimbs, N] NTT form."""
+    c_own = d2_own.clone()
+    engine.intt_(c_own, limb0=shard.lo)
+    c_all = all_gather_limbs(c_own, shard, group)  # the only collective of the whole path
+    return engine.keyswitch_shard(c_all, d2_own, evk_b_own, evk_a_own, shard.lo)

@@ -448,3 +448,45 @@ def crt_centered(x_rns, qs):
         acc = acc + np.asarray(x_rns[i]).astype(object) * (hat * pow(hat % q, -1, q))
     acc = acc % Q
     return np.where(acc > Q // 2, acc - Q, acc)
+
+
+def keyswitch_shard(c_all, d2_own, evk_b_own, evk_a_own, qs, ps, dnum, lo, hi):
+    """One rank's part of the limb-sharded key-switch, restated on the CPU.
+
+    c_all: (L, N) coefficient form of all of d2 (after the all-gather); d2_own: (hi - lo, N) NTT
+    form of Q-limbs [lo, hi); evk_*_own: (dnum, hi - lo + K, N) rows = own Q-limbs then P-limbs.
+    Uses nothing but these inputs; returns (ks0, ks1) for limbs [lo, hi), NTT form."""
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    L, K = len(qs), len(ps)
+    rows = list(range(lo, hi)) + list(range(L, L + K))
+    allm = qs + ps
+    rmods = [allm[t] for t in rows]
+    n = np.asarray(c_all).shape[-1]
+    c_all = np.asarray(c_all).astype(object)
+    acc0 = np.zeros((len(rows), n), dtype=object)
+    acc1 = np.zeros_like(acc0)
+    col = _mods_col(rmods)
+    for j, (dlo, dhi) in enumerate(digit_ranges(L, dnum)):
+        others = [t for t in rows if not dlo <= t < dhi]
+        conv = baseconv(c_all[dlo:dhi], qs[dlo:dhi], [allm[t] for t in others]) if others else []
+        convn = rns_ntt_fwd(conv, [allm[t] for t in others]) if others else []
+        ext = np.empty((len(rows), n), dtype=object)
+        k = 0
+        for r, t in enumerate(rows):
+            if dlo <= t < dhi:
+                ext[r] = np.asarray(d2_own[r]).astype(object)
+            else:
+                ext[r] = convn[k]
+                k += 1
+        acc0 = (acc0 + ext * np.asarray(evk_b_own[j]).astype(object)) % col
+        acc1 = (acc1 + ext * np.asarray(evk_a_own[j]).astype(object)) % col
+    nq = hi - lo
+    P = math.prod(ps)
+    outs = []
+    for acc in (acc0, acc1):
+        xp = rns_ntt_inv(acc[nq:], ps)
+        conv = rns_ntt_fwd(baseconv(xp, ps, qs[lo:hi]), qs[lo:hi])
+        outs.append(np.stack([(acc[i] - conv[i]) * pow(P % q, -1, q) % q
+                              for i, q in enumerate(qs[lo:hi])]))
+    return outs[0], outs[1]

@@ -1,0 +1,125 @@
+"""Multi-rank (gloo, world_size 2 and 4, CPU) tests of the RNS-limb sharding orchestration in
+fhecore/dist.py: the same code drives the HIP Context on MI355X ranks over RCCL.  The engine here
+is a CPU restatement (oracle/, test infrastructure) with the Context's method signatures."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import coracle
+import pyoracle
+from fhecore.dist import LimbShard, all_gather_limbs, sharded_hommult, sharded_keyswitch
+
+LOG_N, L, K, DNUM = 6, 4, 2, 2
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64))
+
+
+def _a(t):
+    return t.contiguous().numpy().view(np.uint64)
+
+
+class CpuEngine:
+    """Context-shaped CPU engine over the oracle (torch int64 CPU tensors)."""
+
+    def __init__(self, qs, ps):
+        self.qs, self.ps = list(qs), list(ps)
+
+    def intt_(self, t, limb0=0):
+        nl = t.shape[-2]
+        t.copy_(_t(coracle.ntt_inv(_a(t), self.qs[limb0:limb0 + nl])))
+        return t
+
+    def hommult(self, a, b, out=None, limb0=0, workspace=None):
+        nl = a.shape[-2]
+        return _t(coracle.hommult(_a(a), _a(b), self.qs[limb0:limb0 + nl]))
+
+    def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0):
+        nl = d2_own.shape[-2]
+        k0, k1 = pyoracle.keyswitch_shard(_a(c_all), _a(d2_own), _a(evk_b), _a(evk_a), self.qs,
+                                          self.ps, DNUM, limb0, limb0 + nl)
+        return _t(k0.astype(np.uint64)), _t(k1.astype(np.uint64))
+
+
+def _data(seed=0):
+    mods = pyoracle.gen_moduli(LOG_N, L + K)
+    qs, ps = mods[:L], mods[L:]
+    rng = np.random.default_rng(seed)
+    n = 1 << LOG_N
+    rand = lambda ms, lead: np.stack([rng.integers(0, q, lead + (n,), dtype=np.uint64) for q in ms],  # noqa: E731
+                                     axis=len(lead))
+    d2 = rand(qs, ())
+    eb, ea = rand(mods, (DNUM,)), rand(mods, (DNUM,))
+    a, b = rand(qs, (3, 2)), rand(qs, (3, 2))
+    return qs, ps, d2, eb, ea, a, b
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        qs, ps, d2, eb, ea, a, b = _data()
+        shard = LimbShard.from_env(L)
+        eng = CpuEngine(qs, ps)
+        rows = shard.evk_rows(K)
+        k0, k1 = sharded_keyswitch(eng, _t(d2[shard.lo:shard.hi]), _t(eb[:, rows]),
+                                   _t(ea[:, rows]), shard)
+        d = sharded_hommult(eng, _t(a[:, :, shard.lo:shard.hi]), _t(b[:, :, shard.lo:shard.hi]),
+                            shard)
+        g0 = all_gather_limbs(k0, shard)
+        g1 = all_gather_limbs(k1, shard)
+        dd = [torch.empty_like(d) for _ in range(world)]
+        dist.all_gather(dd, d)
+        if rank == 0:
+            q.put((_a(g0).copy(), _a(g1).copy(), np.concatenate([_a(x) for x in dd], axis=2)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_keyswitch_and_hommult_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    g0, g1, d = q.get()
+    qs, ps, d2, eb, ea, a, b = _data()
+    r0, r1 = coracle.keyswitch(d2, eb, ea, qs, ps, DNUM)
+    assert (g0 == r0).all() and (g1 == r1).all()
+    assert (d == coracle.hommult(a, b, qs)).all()
+
+
+def test_limb_shard_ranges():
+    s = LimbShard(16, 8, 3)
+    assert (s.lo, s.hi, s.nlimbs) == (6, 8, 2)
+    assert s.evk_rows(4) == [6, 7, 16, 17, 18, 19]
+    with pytest.raises(ValueError):
+        LimbShard(10, 4, 0)
+    x = torch.arange(16 * 3).reshape(16, 3)
+    assert s.own(x).tolist() == x[6:8].tolist()
+
+
+def test_single_rank_shard_is_identity():
+    qs, ps, d2, eb, ea, a, b = _data(1)
+    shard = LimbShard(L, 1, 0)
+    eng = CpuEngine(qs, ps)
+    k0, k1 = sharded_keyswitch(eng, _t(d2), _t(eb), _t(ea), shard)
+    r0, r1 = coracle.keyswitch(d2, eb, ea, qs, ps, DNUM)
+    assert (_a(k0) == r0).all() and (_a(k1) == r1).all()

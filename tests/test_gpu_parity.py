@@ -279,3 +279,18 @@ def test_bad_window_is_rejected(fc):
     t = fc.to_device(np.zeros((1, 2, 4096), np.uint64))
     with pytest.raises(fc.FheError):
         ctx.ntt_(t)  # 2 limbs on a 1-limb context
+
+
+def test_dist_sharded_keyswitch_single_rank_on_gpu(fc):
+    """fhecore.dist driving the HIP Context (world 1: the all-gather is the identity)."""
+    from fhecore.dist import LimbShard, sharded_keyswitch
+
+    L, K, dnum = 8, 2, 3
+    ctx = ctx_for(fc, 14, L, K=K, dnum=dnum)
+    d2 = rand(ctx.moduli, 14, seed=80)
+    eb = rand(ctx.all_moduli, 14, (dnum,), seed=81)
+    ea = rand(ctx.all_moduli, 14, (dnum,), seed=82)
+    k0, k1 = sharded_keyswitch(ctx, fc.to_device(d2), fc.to_device(eb), fc.to_device(ea),
+                               LimbShard(L, 1, 0))
+    r0, r1 = coracle.keyswitch(d2, eb, ea, ctx.moduli, ctx.special, dnum)
+    assert (fc.to_host(k0) == r0).all() and (fc.to_host(k1) == r1).all()
