@@ -249,10 +249,10 @@ def run_keyswitch(args, world, rank):
     evk_b = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
     evk_a = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
     B = args.batch
-    d2 = [uniform_limbs(gen, ctx.moduli[shard.lo:shard.hi], (), n) for _ in range(B)]
-    ws = ctx.workspace(load().fhe_keyswitch_workspace(ctx.handle, shard.nlimbs))
+    d2 = uniform_limbs(gen, ctx.moduli[shard.lo:shard.hi], (B,), n)
+    ws = ctx.workspace(load().fhe_keyswitch_workspace(ctx.handle, shard.nlimbs, B))
 
-    class Eng:  # Context with a shared workspace
+    class Eng:  # the Context, with a preallocated workspace
         intt_ = ctx.intt_
 
         @staticmethod
@@ -260,13 +260,13 @@ def run_keyswitch(args, world, rank):
             return ctx.keyswitch_shard(c_all, d2_own, eb, ea, limb0, workspace=ws)
 
     def step():
-        for j in range(B):
-            fdist.sharded_keyswitch(Eng, d2[j], evk_b, evk_a, shard)
+        fdist.sharded_keyswitch(Eng, d2, evk_b, evk_a, shard)
 
-    dt, kavg = timed(step, args, world, 64 * B * args.steps + 64)
+    dt, kavg = timed(step, args, world, 64 * args.steps + 64)
     ks_per_s = B * args.steps / dt
-    # d2 in + evk (dnum * 2 * (L + K) limbs) + 2 L limbs out, unsharded, per key-switch
-    alg = (L + dnum * 2 * (L + K) + 2 * L) * n * 8
+    # d2 in + evk (dnum * 2 * (L + K) limbs) + 2 L limbs out per key-switch; the
+    # key is shared by the batch, so per batch: B (d2 + out) + one key, unsharded
+    alg = (B * 3 * L + dnum * 2 * (L + K)) * n * 8 // B
     gbps = ks_per_s * alg / 1e9 / world
     dom = max(kavg, key=kavg.get)
     out = {"metric": "key-switches/sec at N=2^16, L=16, K=4, dnum=4 (RNS limbs sharded, RCCL all-gather)",

@@ -206,32 +206,35 @@ int fhe_baseconv(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t s
   return launch_baseconv(c, out, in, s0, S, t0, T, hs(s));
 }
 
-size_t fhe_keyswitch_workspace(const fhe_ctx* c, uint32_t nlimbs) {
-  return c ? keyswitch_workspace_bytes(c, nlimbs) : 0;
+size_t fhe_keyswitch_workspace(const fhe_ctx* c, uint32_t nlimbs, uint32_t batch) {
+  return c ? keyswitch_workspace_bytes(c, nlimbs, batch) : 0;
 }
 
 int fhe_keyswitch_shard(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t* c_all,
                         const uint64_t* d2_own, const uint64_t* evk_b, const uint64_t* evk_a,
-                        uint32_t limb0, uint32_t nlimbs, void* ws, fhe_stream_t s) {
+                        uint32_t limb0, uint32_t nlimbs, uint32_t batch, void* ws,
+                        fhe_stream_t s) {
   int rc = check_window(c, limb0, nlimbs, c ? c->L : 0, "fhe_keyswitch_shard");
   if (rc) return rc;
-  if ((rc = ensure_ws(c, keyswitch_workspace_bytes(c, nlimbs), &ws))) return rc;
-  return launch_keyswitch_shard(c, ks0, ks1, c_all, d2_own, evk_b, evk_a, limb0, nlimbs, ws,
-                                hs(s));
+  if ((rc = ensure_ws(c, keyswitch_workspace_bytes(c, nlimbs, batch), &ws))) return rc;
+  return launch_keyswitch_shard(c, ks0, ks1, c_all, d2_own, evk_b, evk_a, limb0, nlimbs, batch,
+                                ws, hs(s));
 }
 
 int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t* d2,
-                  const uint64_t* evk_b, const uint64_t* evk_a, void* ws, fhe_stream_t s) {
+                  const uint64_t* evk_b, const uint64_t* evk_a, uint32_t batch, void* ws,
+                  fhe_stream_t s) {
   int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_keyswitch");
   if (rc) return rc;
-  if ((rc = ensure_ws(c, keyswitch_workspace_bytes(c, c->L), &ws))) return rc;
+  const size_t bytes = keyswitch_workspace_bytes(c, c->L, batch);
+  if ((rc = ensure_ws(c, bytes, &ws))) return rc;
   // c_all = INTT(d2) lives at the tail of the workspace
-  const size_t tail = keyswitch_workspace_bytes(c, c->L) - (size_t)c->L * c->n * sizeof(uint64_t);
-  uint64_t* c_all = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + tail);
-  FHE_HIP_CHECK(hipMemcpyAsync(c_all, d2, (size_t)c->L * c->n * sizeof(uint64_t),
-                               hipMemcpyDeviceToDevice, hs(s)));
-  if ((rc = launch_ntt(c, false, c_all, c_all, 1, 0, 0, c->L, hs(s)))) return rc;
-  return launch_keyswitch_shard(c, ks0, ks1, c_all, d2, evk_b, evk_a, 0, c->L, ws, hs(s));
+  const size_t call = (size_t)batch * c->L * c->n * sizeof(uint64_t);
+  uint64_t* c_all = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + bytes - call);
+  FHE_HIP_CHECK(hipMemcpyAsync(c_all, d2, call, hipMemcpyDeviceToDevice, hs(s)));
+  if ((rc = launch_ntt(c, false, c_all, c_all, batch, (uint64_t)c->L * c->n, 0, c->L, hs(s))))
+    return rc;
+  return launch_keyswitch_shard(c, ks0, ks1, c_all, d2, evk_b, evk_a, 0, c->L, batch, ws, hs(s));
 }
 
 }  // extern "C"

@@ -72,14 +72,14 @@ int launch_vec_mod(int op, u64* out, const u64* a, const u64* b, u64 rows, u64 c
                    const ModParams* d_mods, u64 mod_stride, int signed_in, hipStream_t s);
 
 // ---- launchers (rns.hip) --------------------------------------------------------------
-// Per-rank body of the hybrid key-switch (SURVEY.md §8a', §8e): c_all [L][N] coefficient form of
-// the whole d2 (all-gathered), d2_own [nlimbs][N] NTT form of this rank's Q-limbs
-// [limb0, limb0 + nlimbs), evk_b/evk_a [dnum][nlimbs + K][N] NTT form (own Q-limbs then P).
-// ks0/ks1 [nlimbs][N] NTT form.
+// Per-rank body of the hybrid key-switch (SURVEY.md §8a', §8e) over `batch` ciphertexts sharing
+// one key: c_all [batch][L][N] coefficient form of the whole d2 (all-gathered), d2_own
+// [batch][nlimbs][N] NTT form of this rank's Q-limbs [limb0, limb0 + nlimbs), evk_b/evk_a
+// [dnum][nlimbs + K][N] NTT form (own Q-limbs then P).  ks0/ks1 [batch][nlimbs][N] NTT form.
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_all,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
-                           u32 nlimbs, void* ws, hipStream_t s);
-size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs);
+                           u32 nlimbs, u32 batch, void* ws, hipStream_t s);
+size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch);
 // Fast basis extension between contiguous ctx limb ranges: in [S][N] over limbs [s0, s0+S),
 // out [T][N] over limbs [t0, t0+T) (ranges disjoint).
 int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u32 t0, u32 T,

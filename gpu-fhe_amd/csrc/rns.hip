@@ -35,16 +35,19 @@ inline ulonglong2 shoup_pair(u64 w, u64 q) {
 
 // in: S rows (stride N) over ctx limbs src0..src0+S-1; out: T rows (stride N), row r over
 // ctx limb map.limb(r); rows whose limb lies in [skip_lo, skip_hi) are left untouched.
-// inv[k] = (S^_k)^-1 mod s_k; hat[k * hs + limb] = S^_k mod limb.
+// inv[k] = (S^_k)^-1 mod s_k; hat[k * hs + limb] = S^_k mod limb.  Batch b = blockIdx.y reads
+// in + b * in_bs and writes out + b * out_bs.
 template <int S>
-__global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ in, u32 src0,
-                                                       u64* __restrict__ out, u32 T, RowMap map,
-                                                       u32 skip_lo, u32 skip_hi, u64 n,
-                                                       const ulonglong2* __restrict__ inv,
+__global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ in, u64 in_bs,
+                                                       u32 src0, u64* __restrict__ out, u64 out_bs,
+                                                       u32 T, RowMap map, u32 skip_lo, u32 skip_hi,
+                                                       u64 n, const ulonglong2* __restrict__ inv,
                                                        const ulonglong2* __restrict__ hat, u32 hs,
                                                        const ModParams* __restrict__ mods) {
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  in += (u64)blockIdx.y * in_bs;
+  out += (u64)blockIdx.y * out_bs;
   u64 y[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) {
@@ -66,57 +69,68 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
   }
 }
 
-// acc{0,1}[r][i] = sum_j e_j[r][i] * evk{b,a}[j][r][i] mod t, r over own Q-limbs then P-limbs.
-// e_j = d2_own row when row r's limb is in digit j, else ext[j] row (NTT form).
-__global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0,
-                                                       u64* __restrict__ acc1,
+// acc{0,1}[b][r][i] = sum_j e_j[b][r][i] * evk{b,a}[j][r][i] mod t over own Q-limbs then P-limbs;
+// e_j = d2_own row when row r's limb is in digit j, else ext[j][b] row (NTT form).  Each thread
+// owns one (r, i), holds its 2 * dnum evaluation-key words in registers and walks the batch, so
+// the key -- the dominant traffic of a key-switch -- is read once per batch.
+constexpr int kMaxDnum = 16;
+__global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc, u64 acc_ws,
                                                        const u64* __restrict__ ext,
                                                        const u64* __restrict__ d2_own,
                                                        const u64* __restrict__ evk_b,
                                                        const u64* __restrict__ evk_a, u32 rows,
-                                                       RowMap map, u32 dnum, u32 alpha, u32 L,
-                                                       u64 n, const ModParams* __restrict__ mods) {
+                                                       u32 nq, RowMap map, u32 dnum, u32 alpha,
+                                                       u32 L, u32 batch, u64 n,
+                                                       const ModParams* __restrict__ mods) {
   const u64 total = (u64)rows * n;
   const u64 stride = (u64)gridDim.x * blockDim.x;
+  const u64 rn = (u64)rows * n;
   for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
     const u32 r = (u32)(e / n);
     const u64 i = e % n;
     const u32 limb = map.limb(r);
     const ModParams m = mods[limb];
-    u64 s0 = 0, s1 = 0;
+    const u32 own_digit = limb < L ? limb / alpha : 0xffffffffu;
+    u64 kb[kMaxDnum], ka[kMaxDnum];
     for (u32 j = 0; j < dnum; ++j) {
-      const bool own = limb < L && limb / alpha == j;
-      const u64 x = own ? d2_own[(u64)r * n + i] : ext[((u64)j * rows + r) * n + i];
-      const u64 off = ((u64)j * rows + r) * n + i;
-      s0 = csub(s0 + mulmod_barrett(x, evk_b[off], m), m.q);
-      s1 = csub(s1 + mulmod_barrett(x, evk_a[off], m), m.q);
+      kb[j] = evk_b[(u64)j * rn + e];
+      ka[j] = evk_a[(u64)j * rn + e];
     }
-    acc0[e] = s0;
-    acc1[e] = s1;
+    for (u32 b = 0; b < batch; ++b) {
+      u64 s0 = 0, s1 = 0;
+      for (u32 j = 0; j < dnum; ++j) {
+        const u64 x = j == own_digit ? d2_own[((u64)b * nq + r) * n + i]
+                                     : ext[((u64)j * batch + b) * rn + e];
+        s0 = csub(s0 + mulmod_barrett(x, kb[j], m), m.q);
+        s1 = csub(s1 + mulmod_barrett(x, ka[j], m), m.q);
+      }
+      acc[(u64)b * rn + e] = s0;
+      acc[acc_ws + (u64)b * rn + e] = s1;
+    }
   }
 }
 
-// out{0,1}[r][i] = (acc{0,1}[r][i] - conv{0,1}[r][i]) * P^-1 mod q   (own Q-limbs)
+// out{0,1}[b][r][i] = (acc{0,1}[b][r][i] - conv{0,1}[b][r][i]) * P^-1 mod q over own Q-limbs.
 __global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ out0,
                                                              u64* __restrict__ out1,
-                                                             const u64* __restrict__ acc0,
-                                                             const u64* __restrict__ acc1,
-                                                             u64 acc_pstride,
-                                                             const u64* __restrict__ conv, u32 rows,
-                                                             u32 limb0, u64 n,
+                                                             const u64* __restrict__ acc,
+                                                             u64 acc_ws, u32 rows,
+                                                             const u64* __restrict__ conv,
+                                                             u32 nq, u32 limb0, u32 batch, u64 n,
                                                              const ulonglong2* __restrict__ pinv,
                                                              const ModParams* __restrict__ mods) {
-  const u64 total = (u64)rows * n;
+  const u64 per = (u64)nq * n;
+  const u64 total = (u64)batch * per;
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const u32 limb = limb0 + (u32)(e / n);
+    const u64 b = e / per, ri = e % per;
+    const u32 limb = limb0 + (u32)(ri / n);
     const u64 q = mods[limb].q;
     const ulonglong2 w = pinv[limb];
+    const u64 ai = b * (u64)rows * n + ri;  // acc rows [0, nq) are the own Q-limbs
     const u64 c0 = conv[e], c1 = conv[total + e];
-    const u64 x0 = acc0[e], x1 = acc1[e];
-    (void)acc_pstride;
-    out0[e] = csub(shoup_lazy(x0 + q - c0, w.x, w.y, q), q);
-    out1[e] = csub(shoup_lazy(x1 + q - c1, w.x, w.y, q), q);
+    out0[e] = csub(shoup_lazy(acc[ai] + q - c0, w.x, w.y, q), q);
+    out1[e] = csub(shoup_lazy(acc[acc_ws + ai] + q - c1, w.x, w.y, q), q);
   }
 }
 
@@ -150,22 +164,33 @@ void conv_tables(const std::vector<u64>& mods, u32 s0, u32 S, std::vector<ulongl
   }
 }
 
+// One base conversion launch over `batch` independent inputs (strides in_bs / out_bs words).
+struct BcArgs {
+  const u64* in;
+  u64 in_bs;
+  u32 src0;
+  u64* out;
+  u64 out_bs;
+  u32 T;
+  RowMap map;
+  u32 skip_lo, skip_hi;
+  u32 batch;
+};
+
 template <int S>
-void launch_bc(const u64* in, u32 src0, u64* out, u32 T, RowMap map, u32 skip_lo, u32 skip_hi,
-               u64 n, const ulonglong2* inv, const ulonglong2* hat, u32 hs, const ModParams* mods,
-               hipStream_t s) {
-  const u32 g = (u32)((n + kThreads - 1) / kThreads);
-  k_baseconv<S><<<g, kThreads, 0, s>>>(in, src0, out, T, map, skip_lo, skip_hi, n, inv, hat, hs,
-                                       mods);
+void launch_bc(const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* hat, u32 hs,
+               const ModParams* mods, hipStream_t s) {
+  const dim3 g((u32)((n + kThreads - 1) / kThreads), a.batch);
+  k_baseconv<S><<<g, kThreads, 0, s>>>(a.in, a.in_bs, a.src0, a.out, a.out_bs, a.T, a.map,
+                                       a.skip_lo, a.skip_hi, n, inv, hat, hs, mods);
 }
 
-int baseconv_any(u32 S, const u64* in, u32 src0, u64* out, u32 T, RowMap map, u32 skip_lo,
-                 u32 skip_hi, u64 n, const ulonglong2* inv, const ulonglong2* hat, u32 hs,
-                 const ModParams* mods, hipStream_t s) {
+int baseconv_any(u32 S, const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* hat,
+                 u32 hs, const ModParams* mods, hipStream_t s) {
   switch (S) {
 #define X(k) \
   case k:    \
-    launch_bc<k>(in, src0, out, T, map, skip_lo, skip_hi, n, inv, hat, hs, mods, s); break;
+    launch_bc<k>(a, n, inv, hat, hs, mods, s); break;
     X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #undef X
     default:
@@ -215,66 +240,67 @@ int build_rns_tables(fhe_ctx* c) {
   return kOk;
 }
 
-size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs) {
+size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch) {
   const u64 rows = nlimbs + c->K;
-  // ext [dnum][rows][N] + acc0/acc1 [2][rows][N] + conv [2][nlimbs][N] + c_all [L][N]
-  return ((u64)c->dnum * rows + 2 * rows + 2 * nlimbs + c->L) * c->n * sizeof(u64);
+  // ext [dnum][batch][rows][N] + acc [2][batch][rows][N] + conv [2][batch][nlimbs][N]
+  // + c_all [batch][L][N] (single-device form)
+  return (u64)batch * ((u64)c->dnum * rows + 2 * rows + 2 * nlimbs + c->L) * c->n * sizeof(u64);
 }
 
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_all,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
-                           u32 nlimbs, void* ws, hipStream_t s) {
+                           u32 nlimbs, u32 batch, void* ws, hipStream_t s) {
   if (c->K == 0) {
     set_error("keyswitch: context has no special primes (K = 0)");
     return kInvalid;
   }
+  if (c->dnum > (u32)kMaxDnum) {
+    set_error("keyswitch: dnum > 16");
+    return kUnsupported;
+  }
+  if (batch == 0) return kOk;
   const u32 L = c->L, K = c->K, M = L + K, alpha = c->alpha, rows = nlimbs + K;
-  const u64 n = c->n;
-  u64* ext = static_cast<u64*>(ws);
-  u64* acc = ext + (u64)c->dnum * rows * n;  // [2][rows][N]
-  u64* conv = acc + 2 * (u64)rows * n;       // [2][nlimbs][N]
+  const u64 n = c->n, rn = (u64)rows * n, B = batch;
+  u64* ext = static_cast<u64*>(ws);          // [dnum][B][rows][N]
+  u64* acc = ext + (u64)c->dnum * B * rn;    // [2][B][rows][N]
+  u64* conv = acc + 2 * B * rn;              // [2][B][nlimbs][N]
+  const u64 acc_ws = B * rn;
   const RowMap map{nlimbs, limb0, L};
   int rc;
-  // ModUp + NTT, per digit, for every row not in the digit itself
+  // ModUp + NTT, per digit, for every row outside the digit itself
   for (u32 j = 0; j < c->dnum; ++j) {
     const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
-    u64* e = ext + (u64)j * rows * n;
-    if ((rc = baseconv_any(hi - lo, c_all + (u64)lo * n, lo, e, rows, map, lo, hi, n,
-                           c->d_modup_inv + (size_t)j * alpha, c->d_modup_hat + (size_t)j * alpha * M,
-                           M, c->d_mods, s)))
+    u64* e = ext + (u64)j * B * rn;
+    const BcArgs up{c_all + (u64)lo * n, (u64)L * n, lo, e, rn, rows, map, lo, hi, batch};
+    if ((rc = baseconv_any(hi - lo, up, n, c->d_modup_inv + (size_t)j * alpha,
+                           c->d_modup_hat + (size_t)j * alpha * M, M, c->d_mods, s)))
       return rc;
     // own Q-limbs outside [lo, hi): up to two ranges, then the P-limbs
     const u32 a0 = limb0, a1 = std::min(limb0 + nlimbs, lo);
-    if (a1 > a0 && (rc = launch_ntt(c, true, e, e, 1, 0, a0, a1 - a0, s))) return rc;
+    if (a1 > a0 && (rc = launch_ntt(c, true, e, e, batch, rn, a0, a1 - a0, s))) return rc;
     const u32 b0 = std::max(limb0, hi), b1 = limb0 + nlimbs;
-    if (b1 > b0 &&
-        (rc = launch_ntt(c, true, e + (u64)(b0 - limb0) * n, e + (u64)(b0 - limb0) * n, 1, 0, b0,
-                         b1 - b0, s)))
-      return rc;
-    if ((rc = launch_ntt(c, true, e + (u64)nlimbs * n, e + (u64)nlimbs * n, 1, 0, L, K, s)))
-      return rc;
+    u64* eb = e + (u64)(b0 - limb0) * n;
+    if (b1 > b0 && (rc = launch_ntt(c, true, eb, eb, batch, rn, b0, b1 - b0, s))) return rc;
+    u64* ep = e + (u64)nlimbs * n;
+    if ((rc = launch_ntt(c, true, ep, ep, batch, rn, L, K, s))) return rc;
   }
-  k_ks_inner<<<grid_for((u64)rows * n), kThreads, 0, s>>>(acc, acc + (u64)rows * n, ext, d2_own,
-                                                          evk_b, evk_a, rows, map, c->dnum, alpha,
-                                                          L, n, c->d_mods);
+  k_ks_inner<<<grid_for(rn), kThreads, 0, s>>>(acc, acc_ws, ext, d2_own, evk_b, evk_a, rows,
+                                               nlimbs, map, c->dnum, alpha, L, batch, n, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
+  prof_mark(s, "ks_inner");
   // ModDown: INTT the P rows of both accumulators, convert P -> own Q-limbs, NTT, finish
   u64* accp = acc + (u64)nlimbs * n;
-  if ((rc = launch_ntt(c, false, accp, accp, 2, (u64)rows * n, L, K, s))) return rc;
-  const RowMap qmap{nlimbs, limb0, 0};
-  for (int w = 0; w < 2; ++w) {
-    if ((rc = baseconv_any(K, accp + (u64)w * rows * n, L, conv + (u64)w * nlimbs * n, nlimbs,
-                           qmap, 0, 0, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, s)))
-      return rc;
-  }
-  if ((rc = launch_ntt(c, true, conv, conv, 2, (u64)nlimbs * n, limb0, nlimbs, s))) return rc;
-  // finish: acc rows [0, nlimbs) of acc0 / acc1
-  const u64 total = (u64)nlimbs * n;
-  // acc1 Q-rows live at acc + rows*n; pass via a compact copy-free view: two launches
-  k_moddown_finish<<<grid_for(total), kThreads, 0, s>>>(ks0, ks1, acc, acc + (u64)rows * n, 0,
-                                                        conv, nlimbs, limb0, n, c->d_pinv,
-                                                        c->d_mods);
+  if ((rc = launch_ntt(c, false, accp, accp, 2 * batch, rn, L, K, s))) return rc;
+  const BcArgs down{accp, rn, L, conv, (u64)nlimbs * n, nlimbs, RowMap{nlimbs, limb0, 0}, 0, 0,
+                    2 * batch};
+  if ((rc = baseconv_any(K, down, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, s)))
+    return rc;
+  if ((rc = launch_ntt(c, true, conv, conv, 2 * batch, (u64)nlimbs * n, limb0, nlimbs, s)))
+    return rc;
+  k_moddown_finish<<<grid_for(B * nlimbs * n), kThreads, 0, s>>>(
+      ks0, ks1, acc, acc_ws, rows, conv, nlimbs, limb0, batch, n, c->d_pinv, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
+  prof_mark(s, "moddown_finish");
   return kOk;
 }
 
@@ -292,8 +318,8 @@ int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u3
   FHE_HIP_CHECK(hipMemcpyAsync(d_tab, inv.data(), inv.size() * 16, hipMemcpyHostToDevice, s));
   FHE_HIP_CHECK(hipMemcpyAsync(d_tab + inv.size(), hat.data(), hat.size() * 16,
                                hipMemcpyHostToDevice, s));
-  const int rc = baseconv_any(S, in, s0, out, T, RowMap{T, t0, 0}, 0, 0, c->n, d_tab,
-                              d_tab + inv.size(), M, c->d_mods, s);
+  const BcArgs a{in, 0, s0, out, 0, T, RowMap{T, t0, 0}, 0, 0, 1};
+  const int rc = baseconv_any(S, a, c->n, d_tab, d_tab + inv.size(), M, c->d_mods, s);
   // the host vectors must outlive the async copies
   FHE_HIP_CHECK(hipStreamSynchronize(s));
   FHE_HIP_CHECK(hipFreeAsync(d_tab, s));

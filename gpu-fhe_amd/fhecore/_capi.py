@@ -41,9 +41,10 @@ SIGNATURES = {
     "fhe_hommult_workspace": (_sz, [_vp, _u32, _u32]),
     "fhe_hommult": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
     "fhe_baseconv": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _vp]),
-    "fhe_keyswitch_workspace": (_sz, [_vp, _u32]),
-    "fhe_keyswitch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "fhe_keyswitch_shard": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
+    "fhe_keyswitch_workspace": (_sz, [_vp, _u32, _u32]),
+    "fhe_keyswitch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
+    "fhe_keyswitch_shard": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp,
+                                   _vp]),
     "fhe_prof_begin": (_i32, [_u32, _vp]),
     "fhe_prof_end": (_i32, [ctypes.POINTER(ctypes.c_float), _u32, ctypes.POINTER(_u32),
                             ctypes.c_char_p, _sz]),

@@ -217,28 +217,41 @@ class Context:
         return out
 
     def keyswitch(self, d2, evk_b, evk_a, workspace=None):
-        """d2 [L, N] NTT form; evk_b/evk_a [dnum, L + K, N] NTT form -> (ks0, ks1) [L, N] NTT form."""
+        """d2 [L, N] or [batch, L, N] NTT form; evk_b/evk_a [dnum, L + K, N] NTT form (one key for the
+        whole batch) -> (ks0, ks1) shaped like d2, NTT form."""
         for t, nm in ((d2, "d2"), (evk_b, "evk_b"), (evk_a, "evk_a")):
             _check_tensor(t, nm, (self.n,))
         if tuple(evk_b.shape) != (self.dnum, self.L + self.K, self.n) or evk_a.shape != evk_b.shape:
             raise ValueError("keyswitch: evk must be [dnum, L + K, N]")
-        ks0, ks1 = self.empty(self.L, self.n), self.empty(self.L, self.n)
+        if d2.shape[-2] != self.L:
+            raise ValueError("keyswitch: d2 must be [..., L, N]")
+        batch = d2.numel() // (self.L * self.n)
+        ks0, ks1 = torch.empty_like(d2), torch.empty_like(d2)
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
-            lib.fhe_keyswitch_workspace(self._ptr, self.L))
+            lib.fhe_keyswitch_workspace(self._ptr, self.L, batch))
         with torch.cuda.device(self.device):
             check(lib.fhe_keyswitch(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(d2), _ptr(evk_b),
-                                    _ptr(evk_a), _ptr(ws), _stream(d2)), "fhe_keyswitch")
+                                    _ptr(evk_a), batch, _ptr(ws), _stream(d2)), "fhe_keyswitch")
         return ks0, ks1
 
     def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0: int, workspace=None):
+        """One rank's key-switch (see fhecore.dist): c_all [..., L, N] coefficient form,
+        d2_own [..., nlimbs, N] NTT form, evk slices [dnum, nlimbs + K, N]."""
+        for t, nm in ((c_all, "c_all"), (d2_own, "d2_own"), (evk_b, "evk_b"), (evk_a, "evk_a")):
+            _check_tensor(t, nm, (self.n,))
         nl = d2_own.shape[-2]
-        ks0, ks1 = self.empty(nl, self.n), self.empty(nl, self.n)
+        batch = d2_own.numel() // (nl * self.n)
+        if c_all.numel() != batch * self.L * self.n:
+            raise ValueError("keyswitch_shard: c_all must be [batch, L, N]")
+        if tuple(evk_b.shape) != (self.dnum, nl + self.K, self.n) or evk_a.shape != evk_b.shape:
+            raise ValueError("keyswitch_shard: evk slices must be [dnum, nlimbs + K, N]")
+        ks0, ks1 = torch.empty_like(d2_own), torch.empty_like(d2_own)
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
-            lib.fhe_keyswitch_workspace(self._ptr, nl))
+            lib.fhe_keyswitch_workspace(self._ptr, nl, batch))
         with torch.cuda.device(self.device):
             check(lib.fhe_keyswitch_shard(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(c_all),
                                           _ptr(d2_own), _ptr(evk_b), _ptr(evk_a), limb0, nl,
-                                          _ptr(ws), _stream(d2_own)), "fhe_keyswitch_shard")
+                                          batch, _ptr(ws), _stream(d2_own)), "fhe_keyswitch_shard")
         return ks0, ks1

@@ -64,12 +64,19 @@ class LimbShard:
 
 
 def all_gather_limbs(x_own, shard: LimbShard, group=None):
-    """[nlimbs, N] per rank -> [L, N] on every rank (rank order = limb order)."""
+    """[..., nlimbs, N] per rank -> [..., L, N] on every rank (rank order = limb order).  One
+    all_gather_into_tensor into a [world, ..., nlimbs, N] buffer, then a limb-major reorder."""
     if shard.world == 1:
         return x_own.contiguous()
-    out = torch.empty((shard.L,) + tuple(x_own.shape[1:]), dtype=x_own.dtype, device=x_own.device)
-    dist.all_gather_into_tensor(out, x_own.contiguous(), group=group)
-    return out
+    flat = (shard.world * x_own.shape[0],) + tuple(x_own.shape[1:])
+    buf = torch.empty(flat, dtype=x_own.dtype, device=x_own.device)
+    dist.all_gather_into_tensor(buf, x_own.contiguous(), group=group)
+    if x_own.dim() == 2:
+        return buf  # [world * nlimbs, N] is already limb order
+    buf = buf.view((shard.world,) + tuple(x_own.shape))
+    lead = x_own.dim() - 2
+    perm = list(range(1, lead + 1)) + [0, lead + 1, lead + 2]
+    return buf.permute(perm).reshape(tuple(x_own.shape[:-2]) + (shard.L, x_own.shape[-1])).contiguous()
 
 
 def sharded_hommult(engine, a_own, b_own, shard: LimbShard, out=None, workspace=None):
@@ -80,8 +87,9 @@ def sharded_hommult(engine, a_own, b_own, shard: LimbShard, out=None, workspace=
 def sharded_keyswitch(engine, d2_own, evk_b_own, evk_a_own, shard: LimbShard, group=None):
     """Hybrid key-switch of this rank's limbs (SURVEY.md §8a', §8e).
 
-    d2_own: [nlimbs, N] NTT form (limbs [lo, hi)); evk_*_own: [dnum, nlimbs + K, N] (own Q-limbs then
-    the K P-limbs, see LimbShard.evk_rows).  Returns (ks0_own, ks1_own), [nlimbs, N] NTT form."""
+    d2_own: [..., nlimbs, N] NTT form (limbs [lo, hi), any leading batch shape); evk_*_own:
+    [dnum, nlimbs + K, N] (own Q-limbs then the K P-limbs, see LimbShard.evk_rows), one key for the
+    batch.  Returns (ks0_own, ks1_own) shaped like d2_own, NTT form."""
     c_own = d2_own.clone()
     engine.intt_(c_own, limb0=shard.lo)
     c_all = all_gather_limbs(c_own, shard, group)  # the only collective of the whole path

@@ -118,19 +118,21 @@ int fhe_baseconv(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t
                  uint32_t t0, uint32_t T, fhe_stream_t stream);
 
 /* ---- hybrid key-switch (relinearisation) -------------------------------------------------
- * Single-device form: d2 [L][N] NTT form over Q; evk_b, evk_a [dnum][L + K][N] NTT form over
- * Q u P; ks0, ks1 [L][N] NTT form: ks0 + ks1 s = d2 s'' + small (SURVEY.md §8a').
- * Sharded form (one rank of G): c_all [L][N] = INTT(d2) all-gathered (coefficient form),
- * d2_own [nlimbs][N] NTT form of Q-limbs [limb0, limb0 + nlimbs), evk slices
- * [dnum][nlimbs + K][N] (own Q-limbs then all K P-limbs); outputs [nlimbs][N].  The sharded
- * outputs of G ranks concatenate to the single-device result bit for bit. */
-size_t fhe_keyswitch_workspace(const fhe_ctx* ctx, uint32_t nlimbs);
+ * `batch` ciphertexts share one key.  Single-device form: d2 [batch][L][N] NTT form over Q;
+ * evk_b, evk_a [dnum][L + K][N] NTT form over Q u P; ks0, ks1 [batch][L][N] NTT form:
+ * ks0 + ks1 s = d2 s'' + small (SURVEY.md §8a').  The key is read once per batch.
+ * Sharded form (one rank of G): c_all [batch][L][N] = INTT(d2) all-gathered (coefficient form),
+ * d2_own [batch][nlimbs][N] NTT form of Q-limbs [limb0, limb0 + nlimbs), evk slices
+ * [dnum][nlimbs + K][N] (own Q-limbs then all K P-limbs); outputs [batch][nlimbs][N].  The
+ * sharded outputs of G ranks concatenate to the single-device result bit for bit. */
+size_t fhe_keyswitch_workspace(const fhe_ctx* ctx, uint32_t nlimbs, uint32_t batch);
 int fhe_keyswitch(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const uint64_t* d2,
-                  const uint64_t* evk_b, const uint64_t* evk_a, void* workspace,
+                  const uint64_t* evk_b, const uint64_t* evk_a, uint32_t batch, void* workspace,
                   fhe_stream_t stream);
 int fhe_keyswitch_shard(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const uint64_t* c_all,
                         const uint64_t* d2_own, const uint64_t* evk_b, const uint64_t* evk_a,
-                        uint32_t limb0, uint32_t nlimbs, void* workspace, fhe_stream_t stream);
+                        uint32_t limb0, uint32_t nlimbs, uint32_t batch, void* workspace,
+                        fhe_stream_t stream);
 
 /* ---- timing marks (measurement support, not part of the reference surface) ------------------
  * fhe_prof_begin records a HIP event on `stream`, then every kernel this host thread launches

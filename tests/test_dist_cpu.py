@@ -42,9 +42,12 @@ class CpuEngine:
 
     def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0):
         nl = d2_own.shape[-2]
-        k0, k1 = pyoracle.keyswitch_shard(_a(c_all), _a(d2_own), _a(evk_b), _a(evk_a), self.qs,
-                                          self.ps, DNUM, limb0, limb0 + nl)
-        return _t(k0.astype(np.uint64)), _t(k1.astype(np.uint64))
+        ca, da = _a(c_all).reshape(-1, L, 1 << LOG_N), _a(d2_own).reshape(-1, nl, 1 << LOG_N)
+        outs = [pyoracle.keyswitch_shard(c, d, _a(evk_b), _a(evk_a), self.qs, self.ps, DNUM, limb0,
+                                         limb0 + nl) for c, d in zip(ca, da)]
+        k0 = np.stack([o[0] for o in outs]).astype(np.uint64).reshape(d2_own.shape)
+        k1 = np.stack([o[1] for o in outs]).astype(np.uint64).reshape(d2_own.shape)
+        return _t(k0), _t(k1)
 
 
 def _data(seed=0):
@@ -54,7 +57,7 @@ def _data(seed=0):
     n = 1 << LOG_N
     rand = lambda ms, lead: np.stack([rng.integers(0, q, lead + (n,), dtype=np.uint64) for q in ms],  # noqa: E731
                                      axis=len(lead))
-    d2 = rand(qs, ())
+    d2 = rand(qs, (2,))  # a batch of two ciphertexts sharing one key
     eb, ea = rand(mods, (DNUM,)), rand(mods, (DNUM,))
     a, b = rand(qs, (3, 2)), rand(qs, (3, 2))
     return qs, ps, d2, eb, ea, a, b
@@ -68,7 +71,7 @@ def _worker(rank, world, port, q):
         shard = LimbShard.from_env(L)
         eng = CpuEngine(qs, ps)
         rows = shard.evk_rows(K)
-        k0, k1 = sharded_keyswitch(eng, _t(d2[shard.lo:shard.hi]), _t(eb[:, rows]),
+        k0, k1 = sharded_keyswitch(eng, _t(d2[:, shard.lo:shard.hi]), _t(eb[:, rows]),
                                    _t(ea[:, rows]), shard)
         d = sharded_hommult(eng, _t(a[:, :, shard.lo:shard.hi]), _t(b[:, :, shard.lo:shard.hi]),
                             shard)
@@ -101,8 +104,9 @@ def test_sharded_keyswitch_and_hommult_gloo(world):
         assert p.exitcode == 0
     g0, g1, d = q.get()
     qs, ps, d2, eb, ea, a, b = _data()
-    r0, r1 = coracle.keyswitch(d2, eb, ea, qs, ps, DNUM)
-    assert (g0 == r0).all() and (g1 == r1).all()
+    for i in range(2):
+        r0, r1 = coracle.keyswitch(d2[i], eb, ea, qs, ps, DNUM)
+        assert (g0[i] == r0).all() and (g1[i] == r1).all()
     assert (d == coracle.hommult(a, b, qs)).all()
 
 
@@ -121,5 +125,6 @@ def test_single_rank_shard_is_identity():
     shard = LimbShard(L, 1, 0)
     eng = CpuEngine(qs, ps)
     k0, k1 = sharded_keyswitch(eng, _t(d2), _t(eb), _t(ea), shard)
-    r0, r1 = coracle.keyswitch(d2, eb, ea, qs, ps, DNUM)
-    assert (_a(k0) == r0).all() and (_a(k1) == r1).all()
+    for i in range(2):
+        r0, r1 = coracle.keyswitch(d2[i], eb, ea, qs, ps, DNUM)
+        assert (_a(k0)[i] == r0).all() and (_a(k1)[i] == r1).all()
