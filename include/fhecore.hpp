@@ -1,0 +1,183 @@
+// fhecore.hpp -- header-only C++ Context / Ciphertext / Evaluator over the libfhecore C ABI.
+//
+// north_star asks for a C++ ciphertext/context/evaluator API in front of the NTT/modmul hot path.
+// The reference has none (it is module-level Python, /root/reference/arithmetic.py:3-19), so this
+// layer is build-defined: RAII ownership of the context and of device buffers, ciphertexts as
+// [components][limbs][N] uint64 device arrays, and an Evaluator whose methods map 1:1 to the
+// C entry points (include/fhecore.h).  Errors become fhe::Error exceptions carrying
+// fhe_last_error().  Requires the HIP runtime (hipMalloc/hipMemcpy) and -lfhecore.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "fhecore.h"
+
+namespace fhe {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+inline void check(int rc, const char* what) {
+  if (rc != FHE_OK) throw Error(rc, std::string(what) + ": " + fhe_last_error());
+}
+
+inline void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw Error(FHE_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Owning device array of uint64 words.
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(size_t words) : n_(words) {
+    if (n_) check_hip(hipMalloc(reinterpret_cast<void**>(&p_), n_ * 8), "hipMalloc");
+  }
+  ~DeviceBuffer() {
+    if (p_) (void)hipFree(p_);
+  }
+  DeviceBuffer(DeviceBuffer&& o) noexcept : p_(std::exchange(o.p_, nullptr)), n_(std::exchange(o.n_, 0)) {}
+  DeviceBuffer& operator=(DeviceBuffer&& o) noexcept {
+    std::swap(p_, o.p_);
+    std::swap(n_, o.n_);
+    return *this;
+  }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+
+  uint64_t* data() const { return p_; }
+  size_t size() const { return n_; }
+  void upload(const std::vector<uint64_t>& h) {
+    if (h.size() != n_) throw Error(FHE_EINVAL, "upload: size mismatch");
+    check_hip(hipMemcpy(p_, h.data(), n_ * 8, hipMemcpyHostToDevice), "hipMemcpy H2D");
+  }
+  std::vector<uint64_t> download() const {
+    std::vector<uint64_t> h(n_);
+    check_hip(hipMemcpy(h.data(), p_, n_ * 8, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+    return h;
+  }
+
+ private:
+  uint64_t* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+// RNS parameters + device tables (fhe_ctx).  Immutable once built.
+class Context {
+ public:
+  Context(uint32_t log_n, const std::vector<uint64_t>& q, const std::vector<uint64_t>& p = {},
+          uint32_t dnum = 1, int device = 0)
+      : log_n_(log_n), L_((uint32_t)q.size()), K_((uint32_t)p.size()) {
+    check(fhe_ctx_create(&c_, log_n, q.data(), L_, p.empty() ? nullptr : p.data(), K_,
+                         K_ ? dnum : 0, device),
+          "fhe_ctx_create");
+  }
+  // The SURVEY.md §8a' chain: L + K largest 60-bit NTT primes for N = 2^log_n.
+  static Context standard(uint32_t log_n, uint32_t L, uint32_t K = 0, uint32_t dnum = 1,
+                          int device = 0) {
+    std::vector<uint64_t> m(L + K);
+    check(fhe_gen_moduli(log_n, L + K, 60, 0, m.data()), "fhe_gen_moduli");
+    return Context(log_n, std::vector<uint64_t>(m.begin(), m.begin() + L),
+                   std::vector<uint64_t>(m.begin() + L, m.end()), dnum, device);
+  }
+  ~Context() {
+    if (c_) fhe_ctx_destroy(c_);
+  }
+  Context(Context&& o) noexcept
+      : c_(std::exchange(o.c_, nullptr)), log_n_(o.log_n_), L_(o.L_), K_(o.K_) {}
+  Context(const Context&) = delete;
+  Context& operator=(const Context&) = delete;
+
+  const fhe_ctx* get() const { return c_; }
+  uint32_t log_n() const { return log_n_; }
+  uint64_t n() const { return 1ull << log_n_; }
+  uint32_t L() const { return L_; }
+  uint32_t K() const { return K_; }
+
+ private:
+  fhe_ctx* c_ = nullptr;
+  uint32_t log_n_, L_, K_;
+};
+
+// A ciphertext (or plain polynomial when components == 1): [components][limbs][N] residues.
+struct Ciphertext {
+  uint32_t components = 0, limbs = 0;
+  uint64_t n = 0;
+  bool ntt_form = false;
+  DeviceBuffer buf;
+  Ciphertext() = default;
+  Ciphertext(const Context& ctx, uint32_t comps, uint32_t nlimbs, bool ntt = false)
+      : components(comps), limbs(nlimbs), n(ctx.n()), ntt_form(ntt), buf((size_t)comps * nlimbs * ctx.n()) {}
+  uint64_t* data() const { return buf.data(); }
+};
+
+// Homomorphic operations on one stream.
+class Evaluator {
+ public:
+  explicit Evaluator(const Context& ctx, hipStream_t stream = nullptr) : ctx_(ctx), s_(stream) {}
+
+  void ntt(Ciphertext& x) const {
+    check(fhe_ntt_fwd(ctx_.get(), x.data(), x.components, 0, x.limbs, s_), "fhe_ntt_fwd");
+    x.ntt_form = true;
+  }
+  void intt(Ciphertext& x) const {
+    check(fhe_ntt_inv(ctx_.get(), x.data(), x.components, 0, x.limbs, s_), "fhe_ntt_inv");
+    x.ntt_form = false;
+  }
+  void add(Ciphertext& out, const Ciphertext& a, const Ciphertext& b) const {
+    same(a, b, "add");
+    check(fhe_vec_add(ctx_.get(), out.data(), a.data(), b.data(), a.components, 0, a.limbs, s_),
+          "fhe_vec_add");
+  }
+  void sub(Ciphertext& out, const Ciphertext& a, const Ciphertext& b) const {
+    same(a, b, "sub");
+    check(fhe_vec_sub(ctx_.get(), out.data(), a.data(), b.data(), a.components, 0, a.limbs, s_),
+          "fhe_vec_sub");
+  }
+  // coefficient-wise product (= polynomial product when both are in NTT form)
+  void mul_pointwise(Ciphertext& out, const Ciphertext& a, const Ciphertext& b) const {
+    same(a, b, "mul_pointwise");
+    check(fhe_vec_mul(ctx_.get(), out.data(), a.data(), b.data(), a.components, 0, a.limbs, s_),
+          "fhe_vec_mul");
+  }
+  // ct x ct tensor: (a0, a1) x (b0, b1) -> (d0, d1, d2), coefficient form in and out.
+  Ciphertext multiply(const Ciphertext& a, const Ciphertext& b) const {
+    same(a, b, "multiply");
+    if (a.components != 2 || a.ntt_form) throw Error(FHE_EINVAL, "multiply: need 2-component, coefficient form");
+    Ciphertext d(ctx_, 3, a.limbs);
+    if (ws_.size() * 8 < fhe_hommult_workspace(ctx_.get(), 1, a.limbs))
+      ws_ = DeviceBuffer((fhe_hommult_workspace(ctx_.get(), 1, a.limbs) + 7) / 8);
+    check(fhe_hommult(ctx_.get(), d.data(), a.data(), b.data(), 1, 0, a.limbs, ws_.data(), s_),
+          "fhe_hommult");
+    return d;
+  }
+  // Hybrid key-switch of d2 (NTT form, L limbs) with the key (evk_b, evk_a), NTT form [dnum][L+K][N].
+  std::pair<Ciphertext, Ciphertext> keyswitch(const Ciphertext& d2, const DeviceBuffer& evk_b,
+                                              const DeviceBuffer& evk_a) const {
+    Ciphertext k0(ctx_, 1, d2.limbs, true), k1(ctx_, 1, d2.limbs, true);
+    const size_t need = fhe_keyswitch_workspace(ctx_.get(), ctx_.L(), 1);
+    if (ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
+    check(fhe_keyswitch(ctx_.get(), k0.data(), k1.data(), d2.data(), evk_b.data(), evk_a.data(), 1,
+                        ws_.data(), s_),
+          "fhe_keyswitch");
+    return {std::move(k0), std::move(k1)};
+  }
+
+ private:
+  static void same(const Ciphertext& a, const Ciphertext& b, const char* who) {
+    if (a.components != b.components || a.limbs != b.limbs || a.n != b.n)
+      throw Error(FHE_EINVAL, std::string(who) + ": shape mismatch");
+  }
+  const Context& ctx_;
+  hipStream_t s_;
+  mutable DeviceBuffer ws_;
+};
+
+}  // namespace fhe

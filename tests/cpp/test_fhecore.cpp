@@ -1,0 +1,73 @@
+// C++ API smoke/parity test (run by tests/test_cpp_api.py on a GPU box): Context / Evaluator from
+// include/fhecore.hpp against a schoolbook negacyclic product computed here with __int128.
+#include <cstdio>
+#include <random>
+
+#include "fhecore.hpp"
+
+using u64 = uint64_t;
+using u128 = unsigned __int128;
+
+static std::vector<u64> negacyclic(const std::vector<u64>& a, const std::vector<u64>& b, u64 q) {
+  const size_t n = a.size();
+  std::vector<u128> acc(n, 0);
+  std::vector<u64> out(n);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) {
+      const u64 p = (u64)((u128)a[i] * b[j] % q);
+      const size_t k = i + j;
+      if (k < n) acc[k] = (acc[k] + p) % q;
+      else acc[k - n] = (acc[k - n] + q - p) % q;
+    }
+  for (size_t i = 0; i < n; ++i) out[i] = (u64)acc[i];
+  return out;
+}
+
+int main() {
+  try {
+    const uint32_t log_n = 10, L = 2;
+    const u64 n = 1ull << log_n;
+    fhe::Context ctx = fhe::Context::standard(log_n, L);
+    std::vector<u64> q(L);
+    fhe::check(fhe_ctx_moduli(ctx.get(), q.data(), nullptr), "moduli");
+    std::mt19937_64 rng(7);
+    std::vector<u64> ha(2 * L * n), hb(2 * L * n);
+    for (uint32_t c = 0; c < 2; ++c)
+      for (uint32_t l = 0; l < L; ++l)
+        for (u64 i = 0; i < n; ++i) {
+          ha[(c * L + l) * n + i] = rng() % q[l];
+          hb[(c * L + l) * n + i] = rng() % q[l];
+        }
+    fhe::Ciphertext a(ctx, 2, L), b(ctx, 2, L);
+    a.buf.upload(ha);
+    b.buf.upload(hb);
+    fhe::Evaluator ev(ctx);
+    fhe::Ciphertext d = ev.multiply(a, b);
+    const std::vector<u64> hd = d.buf.download();
+    for (uint32_t l = 0; l < L; ++l) {
+      auto sl = [&](const std::vector<u64>& v, uint32_t c) {
+        return std::vector<u64>(v.begin() + (c * L + l) * n, v.begin() + (c * L + l + 1) * n);
+      };
+      const auto d0 = negacyclic(sl(ha, 0), sl(hb, 0), q[l]);
+      const auto d2 = negacyclic(sl(ha, 1), sl(hb, 1), q[l]);
+      for (u64 i = 0; i < n; ++i) {
+        if (hd[(0 * L + l) * n + i] != d0[i] || hd[(2 * L + l) * n + i] != d2[i]) {
+          std::printf("FAIL limb %u coeff %llu\n", l, (unsigned long long)i);
+          return 1;
+        }
+      }
+    }
+    // NTT round trip through the Evaluator
+    ev.ntt(a);
+    ev.intt(a);
+    if (a.buf.download() != ha) {
+      std::printf("FAIL ntt round trip\n");
+      return 1;
+    }
+    std::printf("cpp api ok\n");
+    return 0;
+  } catch (const fhe::Error& e) {
+    std::printf("fhe::Error %d: %s\n", e.code, e.what());
+    return 2;
+  }
+}
