@@ -44,6 +44,9 @@ constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per work
 #ifndef FHE_BFLY_ASM
 #define FHE_BFLY_ASM 0
 #endif
+#ifndef FHE_HM_POLY_MAJOR
+#define FHE_HM_POLY_MAJOR 1
+#endif
 #ifndef FHE_NTT_MIN_WAVES
 #define FHE_NTT_MIN_WAVES 1
 #endif
@@ -124,6 +127,28 @@ __device__ __forceinline__ void lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// XCD-aware block -> (limb, rest) split for the row passes.  Their twiddles are per (limb, row):
+// 2 MiB of forward + inverse table per limb, so when every XCD sees every limb the 4 MiB L2 of
+// an XCD thrashes and the re-reads go out to the Infinity Cache (measured: 1.5x the algorithmic
+// read traffic of hm_row_tensor at 8 limbs).  Workgroups are dealt round-robin to the 8 XCDs, so
+// tying the limb to blockIdx % 8 keeps each limb's table on one XCD's L2.  Placement only
+// affects speed: every (limb, rest) pair is still covered exactly once for any nlimbs.
+__device__ __forceinline__ void xcd_limb_split(u32 b, u32 nlimbs, u32& limb, u32& rest) {
+  constexpr u32 kXcd = 8;
+  if (nlimbs % kXcd == 0) {
+    const u32 g = nlimbs / kXcd, hi = b / kXcd;
+    limb = b % kXcd + kXcd * (hi % g);
+    rest = hi / g;
+  } else if (kXcd % nlimbs == 0) {
+    const u32 per = kXcd / nlimbs;  // XCDs per limb
+    limb = (b % kXcd) % nlimbs;
+    rest = (b / kXcd) * per + (b % kXcd) / nlimbs;
+  } else {
+    limb = b % nlimbs;
+    rest = b / nlimbs;
   }
 }
 
@@ -383,9 +408,9 @@ __global__ __launch_bounds__(kThreads) void k_ntt_row(const u64* __restrict__ sr
   using G = Geo<LOGN>;
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[G::LDS_R];
-  const u32 tile = blockIdx.x % G::TILES_R;
-  const u32 pl = blockIdx.x / G::TILES_R;
-  const u32 l = pl % nlimbs, p = pl / nlimbs;
+  u32 l, rest;
+  xcd_limb_split(blockIdx.x, nlimbs, l, rest);
+  const u32 tile = rest % G::TILES_R, p = rest / G::TILES_R;
   const u32 limb = limb0 + l;
   const u32 t = threadIdx.x % G::TPS_R, sub = threadIdx.x / G::TPS_R;
   const u32 row = tile * G::SUBS_R + sub;
@@ -415,7 +440,12 @@ struct HmGeo {
   static constexpr int ROWW = 4 * G::RS;                     // LDS words per row (4 slots)
   static constexpr int TILES = G::R1 / ROWS;
   static_assert(64 % LANES_ROW == 0 || LANES_ROW % 64 == 0, "row group vs wavefront");
-  static constexpr int SYNC = LANES_ROW <= 64 ? kWaveSync : kBlockSync;
+  // FHE_HM_POLY_MAJOR: thread group g = one polynomial spread over whole wavefronts, so during the
+  // 3-poly inverse the 4th group is a whole idle wave (its SIMD slots go to other waves) instead
+  // of idle lanes inside every wave (measured: VALUBusy ~100 % with 77 % lane utilisation).
+  // Exchanges then cross waves and need the block barrier.
+  static constexpr bool POLY_MAJOR = FHE_HM_POLY_MAJOR != 0;
+  static constexpr int SYNC = (!POLY_MAJOR && LANES_ROW <= 64) ? kWaveSync : kBlockSync;
 };
 
 template <int LOGN>
@@ -430,16 +460,23 @@ __global__ __launch_bounds__(kThreads) void k_hommult_row(const u64* __restrict_
   using Rd = Rounds<G::N2>;
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[H::ROWS * H::ROWW];
-  const u32 tile = blockIdx.x % H::TILES;
-  const u32 bl = blockIdx.x / H::TILES;
-  const u32 l = bl % nlimbs, b = bl / nlimbs;
+  u32 l, rest;
+  xcd_limb_split(blockIdx.x, nlimbs, l, rest);
+  const u32 tile = rest % H::TILES, b = rest / H::TILES;
   const u32 limb = limb0 + l;
   const ModParams m = mods[limb];
   const u64 q = m.q;
   const u64 limbN = (u64)nlimbs * N;
-  const u32 sub = threadIdx.x / H::LANES_ROW;
-  const u32 rem = threadIdx.x % H::LANES_ROW;
-  const u32 grp = rem / H::TPS, t = rem % H::TPS;
+  u32 sub, grp, t;
+  if constexpr (H::POLY_MAJOR) {  // [poly][row][lane]
+    grp = threadIdx.x / (H::ROWS * H::TPS);
+    sub = (threadIdx.x / H::TPS) % H::ROWS;
+    t = threadIdx.x % H::TPS;
+  } else {  // [row][poly][lane]
+    sub = threadIdx.x / H::LANES_ROW;
+    grp = (threadIdx.x % H::LANES_ROW) / H::TPS;
+    t = threadIdx.x % H::TPS;
+  }
   const u32 row = tile * H::ROWS + sub;
   const u64 loc = (u64)l * N + (u64)row * G::R2;
   const ulonglong2* tf = twf + (u64)limb * N;

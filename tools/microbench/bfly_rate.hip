@@ -97,6 +97,17 @@ __device__ __forceinline__ u64 csub_mask(u64 x, u64 nm) {
   return (x & msk) | (d & ~msk);
 }
 
+// V5: plain C++ shaped for the compiler: T = x w + h (-q) (one 64-bit add, no borrow),
+// u - 2q via add of -2q and a sign test
+__device__ __forceinline__ u64 shoup5(u64 x, u64 w, u64 ws, u64 nq) {
+  const u64 h = (u64)(((u128)x * ws) >> 64);
+  return x * w + h * nq;
+}
+__device__ __forceinline__ u64 csub5(u64 x, u64 nm) {
+  const u64 d = x + nm;
+  return (int64_t)d < 0 ? x : d;
+}
+
 template <int V>
 __device__ __forceinline__ u64 mulw(u64 x, u64 w, u64 ws, u64 q) {
   if (V == 0) return shoup0(x, w, ws, q);
@@ -123,7 +134,12 @@ __global__ __launch_bounds__(256) void k_bfly(u64* out, const u64* tw, u64 q, in
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
         const int ti = ((1 << (3 - b)) - 1) + (j >> (b + 1));
-        if (V == 4) {
+        if (V == 5) {
+          const u64 u = csub5(x[j], 0 - q2);
+          const u64 v = shoup5(x[jj], w[ti], ws[ti], 0 - q);
+          x[j] = u + v;
+          x[jj] = u - v + q2;
+        } else if (V == 4) {
           const u64 u = csub4(x[j], 0 - q2);
           const u64 v = shoup4(x[jj], w[ti], ws[ti], 0 - q);
           x[j] = u + v;
@@ -189,5 +205,7 @@ int main() {
   run("v3 madchain, lane tw", k_bfly<3, true>, d, tw, q);
   run("v4 asm mads, sgpr tw", k_bfly<4, false>, d, tw, q);
   run("v4 asm mads, lane tw", k_bfly<4, true>, d, tw, q);
+  run("v5 c++ shaped, sgpr tw", k_bfly<5, false>, d, tw, q);
+  run("v5 c++ shaped, lane tw", k_bfly<5, true>, d, tw, q);
   return 0;
 }
