@@ -39,48 +39,26 @@ __device__ __forceinline__ u64 shoup_lazy(u64 x, u64 w, u64 ws, u64 q) {
   return x * w - qh * q;
 }
 
-// ---- pinned-instruction forms for the butterflies --------------------------------------------
+// ---- instruction-shaped forms for the butterflies -------------------------------------------
 // Measured on gfx950 (tools/microbench/isa_rate.hip): v_mad_u64_u32, v_mul_lo/hi_u32 and every
-// 64-bit VALU op (v_lshl_add_u64, v_cmp_*_u64) issue at half the rate of a 32-bit add, and hipcc
-// rewrites low-half-only v_mad_u64_u32 chains into v_mul_lo_u32 + v_add3 and conditional
-// subtractions into compare + select with VCC hazards (s_nop).  These helpers pin the cheaper
-// sequences with inline asm; tools/microbench/bfly_rate.hip measures 43.7 vs 56.9 lane-cycles per
-// butterfly against the plain C++ form.
+// 64-bit VALU op (v_lshl_add_u64, v_cmp_*_u64) issue at half the rate of a 32-bit add.  Left
+// alone, hipcc shrinks v_mad_u64_u32 chains whose high halves it can prove unused into
+// v_mul_lo_u32 + v_add3 + borrow chains, and turns sign-mask selects into 64-bit compares +
+// v_cndmask with VCC hazards (s_nop).  OPAQUE() is an empty asm that makes a value opaque to those
+// rewrites without emitting an instruction (real inline-asm instructions would make the hazard
+// recognizer pad every use).  tools/microbench/bfly_rate.hip: 44 vs 56 lane-cycles per butterfly.
+#define FHE_OPAQUE(x) asm("" : "+v"(x))
 
-// a * b + c (64-bit).
-__device__ __forceinline__ u64 mad_u64_u32(u32 a, u32 b, u64 c) {
-  u64 r, carry_unused;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry_unused) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-// a + b mod 2^64 in one instruction.
-__device__ __forceinline__ u64 add64(u64 a, u64 b) {
-  u64 r;
-  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ u32 bfi32(u32 mask, u32 a, u32 b) {  // (mask & a) | (~mask & b)
-  u32 r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ u32 sign_mask(u32 hi) {  // all ones iff bit 31 set
-  u32 r;
-  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(hi));
-  return r;
-}
-__device__ __forceinline__ u32 not32(u32 x) {
-  u32 r;
-  asm("v_not_b32 %0, %1" : "=v"(r) : "v"(x));
-  return r;
-}
+__device__ __forceinline__ u64 mad_u64_u32(u32 a, u32 b, u64 c) { return (u64)a * b + c; }
 
-// x >= m ? x - m : x for x, m < 2^63, given nm = -m mod 2^64: no compare, no VCC.
+// x >= m ? x - m : x for x, m < 2^63, given nm = -m mod 2^64: sign-mask select (v_bfi_b32).
 __device__ __forceinline__ u64 csub_fast(u64 x, u64 nm) {
-  const u64 d = add64(x, nm);
-  const u32 msk = sign_mask((u32)(d >> 32));
-  return ((u64)bfi32(msk, (u32)(x >> 32), (u32)(d >> 32)) << 32) |
-         bfi32(msk, (u32)x, (u32)d);
+  const u64 d = x + nm;
+  u32 m = (u32)((int32_t)(d >> 32) >> 31);
+  FHE_OPAQUE(m);
+  const u32 lo = ((u32)x & m) | ((u32)d & ~m);
+  const u32 hi = ((u32)(x >> 32) & m) | ((u32)(d >> 32) & ~m);
+  return ((u64)hi << 32) | lo;
 }
 
 // y * w mod q up to one q, y < 2^64, result in [0, 2q): Shoup with the exact quotient
@@ -94,20 +72,26 @@ __device__ __forceinline__ u64 shoup_fast(u64 y, u64 w, u64 ws, u64 nq) {
   const u32 n0 = (u32)nq, n1 = (u32)(nq >> 32);
   const u64 a = mad_u64_u32(y1, s0, __umulhi(y0, s0));
   const u64 b = mad_u64_u32(y0, s1, (u32)a);
-  const u64 h = add64(mad_u64_u32(y1, s1, a >> 32), b >> 32);
+  const u64 h = mad_u64_u32(y1, s1, a >> 32) + (b >> 32);
   const u32 h0 = (u32)h, h1 = (u32)(h >> 32);
-  const u64 t = mad_u64_u32(h0, n0, mad_u64_u32(y0, w0, 0));
+  u64 t = mad_u64_u32(h0, n0, mad_u64_u32(y0, w0, 0));
+  FHE_OPAQUE(t);
   u64 c = mad_u64_u32(y1, w0, t >> 32);
+  FHE_OPAQUE(c);
   c = mad_u64_u32(y0, w1, c);
+  FHE_OPAQUE(c);
   c = mad_u64_u32(h1, n0, c);
+  FHE_OPAQUE(c);
   c = mad_u64_u32(h0, n1, c);
+  FHE_OPAQUE(c);
   return ((u64)(u32)c << 32) | (u32)t;
 }
 
 // a - b + k for a + k > b, with kp1 = k + 1: a + k + 1 + ~b, two 64-bit adds, no borrow chain.
 __device__ __forceinline__ u64 sub_plus(u64 a, u64 b, u64 kp1) {
-  const u64 nb = ((u64)not32((u32)(b >> 32)) << 32) | not32((u32)b);
-  return add64(add64(a, kp1), nb);
+  u64 nb = ~b;
+  FHE_OPAQUE(nb);
+  return (a + kp1) + nb;
 }
 
 // Barrett reduction of a 128-bit z < 4 q^2 into [0, q).

@@ -40,16 +40,24 @@ constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per work
 #ifndef FHE_NTT_ABLATE
 #define FHE_NTT_ABLATE 0
 #endif
-// FHE_BFLY_ASM: butterflies through the inline-asm helpers of modarith.hpp (1) or plain C++ (0).
+// FHE_BFLY_ASM: butterflies through the instruction-shaped helpers of modarith.hpp (1) or the
+// plain C++ Shoup (0).  Shaped wins 20 % in the register-only microbenchmark
+// (tools/microbench/bfly_rate.hip) but ties inside the kernels, where register-pair moves for the
+// mad addends eat the saved instructions (tools/isa_cost.py: 2860 vs 2937 units per column pass).
 #ifndef FHE_BFLY_ASM
 #define FHE_BFLY_ASM 0
 #endif
 #ifndef FHE_HM_POLY_MAJOR
 #define FHE_HM_POLY_MAJOR 1
 #endif
-#ifndef FHE_NTT_MIN_WAVES
-#define FHE_NTT_MIN_WAVES 1
+// FHE_NTT_MAX_WAVES: occupancy the register allocator / scheduler may assume (waves per SIMD).
+// LDS already caps these kernels at 4 workgroups per CU, so a lower target costs no waves and
+// lets the scheduler spend VGPRs on interleaving independent butterflies.
+#ifndef FHE_NTT_MAX_WAVES
+#define FHE_NTT_MAX_WAVES 8
 #endif
+#define FHE_KATTR \
+  __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, FHE_NTT_MAX_WAVES)))
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -189,7 +197,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
 #if FHE_BFLY_ASM
         const u64 u = csub_fast(x[j], nq2);
         const u64 v = shoup_fast(x[jj], w.x, w.y, nq);
-        x[j] = add64(u, v);
+        x[j] = u + v;
         x[jj] = sub_plus(u, v, q2p1);
 #else
         const u64 u = csub(x[j], q2);
@@ -215,7 +223,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         // Harvey GS: inputs in [0, 2q); sum -> [0, 2q); (u - v + 2q) w -> [0, 2q)
         const u64 u = x[j], v = x[jj];
 #if FHE_BFLY_ASM
-        const u64 sum = add64(u, v), dif = sub_plus(u, v, q2p1);
+        const u64 sum = u + v, dif = sub_plus(u, v, q2p1);
 #else
         const u64 sum = u + v, dif = u - v + q2;
 #endif
@@ -369,7 +377,7 @@ struct Geo {
 
 // Column pass. src/dst: [polys][nlimbs][N] via PolyMap; grid = polys * nlimbs * TILES_C.
 template <int LOGN, bool FWD>
-__global__ __launch_bounds__(kThreads) void k_ntt_col(const u64* __restrict__ src,
+__global__ FHE_KATTR void k_ntt_col(const u64* __restrict__ src,
                                                       u64* __restrict__ dst, u32 nlimbs,
                                                       u32 limb0, PolyMap pm,
                                                       const ulonglong2* __restrict__ tw_all,
@@ -400,7 +408,7 @@ __global__ __launch_bounds__(kThreads) void k_ntt_col(const u64* __restrict__ sr
 
 // Row pass. grid = polys * nlimbs * TILES_R.
 template <int LOGN, bool FWD>
-__global__ __launch_bounds__(kThreads) void k_ntt_row(const u64* __restrict__ src,
+__global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
                                                       u64* __restrict__ dst, u32 nlimbs,
                                                       u32 limb0, PolyMap pm,
                                                       const ulonglong2* __restrict__ tw_all,
@@ -449,7 +457,7 @@ struct HmGeo {
 };
 
 template <int LOGN>
-__global__ __launch_bounds__(kThreads) void k_hommult_row(const u64* __restrict__ x,
+__global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
                                                           u64* __restrict__ d, u32 nlimbs,
                                                           u32 limb0,
                                                           const ulonglong2* __restrict__ twf,

@@ -108,6 +108,42 @@ __device__ __forceinline__ u64 csub5(u64 x, u64 nm) {
   return (int64_t)d < 0 ? x : d;
 }
 
+// V6: plain C++ with empty-asm value barriers that stop the compiler from shrinking the mad chain
+// or turning mask selects back into compares (no inline instructions, so no hazard padding)
+#define OPQ(x) asm("" : "+v"(x))
+__device__ __forceinline__ u64 shoup6(u64 y, u64 w, u64 ws, u64 nq) {
+  const u32 y0 = (u32)y, y1 = y >> 32, s0 = (u32)ws, s1 = ws >> 32;
+  const u32 w0 = (u32)w, w1 = w >> 32, n0 = (u32)nq, n1 = nq >> 32;
+  u64 a = mad64(y1, s0, __umulhi(y0, s0));
+  u64 b = mad64(y0, s1, (u32)a);
+  u64 h = mad64(y1, s1, a >> 32) + (b >> 32);
+  const u32 h0 = (u32)h, h1 = h >> 32;
+  u64 t = mad64(y0, w0, 0);
+  t = mad64(h0, n0, t);
+  OPQ(t);
+  u64 c = mad64(y1, w0, t >> 32);
+  OPQ(c);
+  c = mad64(y0, w1, c);
+  OPQ(c);
+  c = mad64(h1, n0, c);
+  OPQ(c);
+  c = mad64(h0, n1, c);
+  OPQ(c);
+  return ((u64)(u32)c << 32) | (u32)t;
+}
+__device__ __forceinline__ u64 csub6(u64 x, u64 nm) {
+  const u64 d = x + nm;
+  u32 m = (u32)((int32_t)(d >> 32) >> 31);
+  OPQ(m);
+  const u32 lo = ((u32)x & m) | ((u32)d & ~m), hi = ((u32)(x >> 32) & m) | ((u32)(d >> 32) & ~m);
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 subp6(u64 u, u64 v, u64 kp1) {
+  u64 nv = ~v;
+  OPQ(nv);
+  return (u + kp1) + nv;
+}
+
 template <int V>
 __device__ __forceinline__ u64 mulw(u64 x, u64 w, u64 ws, u64 q) {
   if (V == 0) return shoup0(x, w, ws, q);
@@ -134,7 +170,12 @@ __global__ __launch_bounds__(256) void k_bfly(u64* out, const u64* tw, u64 q, in
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
         const int ti = ((1 << (3 - b)) - 1) + (j >> (b + 1));
-        if (V == 5) {
+        if (V == 6) {
+          const u64 u = csub6(x[j], 0 - q2);
+          const u64 v = shoup6(x[jj], w[ti], ws[ti], 0 - q);
+          x[j] = u + v;
+          x[jj] = subp6(u, v, q2 + 1);
+        } else if (V == 5) {
           const u64 u = csub5(x[j], 0 - q2);
           const u64 v = shoup5(x[jj], w[ti], ws[ti], 0 - q);
           x[j] = u + v;
@@ -163,17 +204,19 @@ __global__ __launch_bounds__(256) void k_bfly(u64* out, const u64* tw, u64 q, in
   out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
+static size_t g_shmem = 0;  // dynamic LDS per workgroup: limits workgroups (waves) per CU
+
 template <class K>
 static int run(const char* name, K kern, u64* d, const u64* tw, u64 q) {
   const int iters = 256;
   dim3 grid(256 * 16), block(256);
-  kern<<<grid, block>>>(d, tw, q, 2);
+  kern<<<grid, block, g_shmem>>>(d, tw, q, 2);
   CHK(hipDeviceSynchronize());
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
   CHK(hipEventRecord(a));
-  kern<<<grid, block>>>(d, tw, q, iters);
+  kern<<<grid, block, g_shmem>>>(d, tw, q, iters);
   CHK(hipEventRecord(b));
   CHK(hipEventSynchronize(b));
   float ms;
@@ -197,6 +240,14 @@ int main() {
     htw[2 * k + 1] = (u64)(((u128)w << 64) / q);
   }
   CHK(hipMemcpy(tw, htw, sizeof(htw), hipMemcpyHostToDevice));
+  for (size_t sh : {(size_t)34816, (size_t)20000}) {  // 4 and 8 workgroups (waves/SIMD) per CU
+    g_shmem = sh;
+    printf("-- dynamic LDS %zu B per workgroup\n", sh);
+    run("v0 exact, lane tw", k_bfly<0, true>, d, tw, q);
+    run("v6 c++ barriers, lane tw", k_bfly<6, true>, d, tw, q);
+  }
+  g_shmem = 0;
+  printf("-- no LDS limit\n");
   run("v0 exact, sgpr tw", k_bfly<0, false>, d, tw, q);
   run("v0 exact, lane tw", k_bfly<0, true>, d, tw, q);
   run("v1 approx, sgpr tw", k_bfly<1, false>, d, tw, q);
@@ -207,5 +258,7 @@ int main() {
   run("v4 asm mads, lane tw", k_bfly<4, true>, d, tw, q);
   run("v5 c++ shaped, sgpr tw", k_bfly<5, false>, d, tw, q);
   run("v5 c++ shaped, lane tw", k_bfly<5, true>, d, tw, q);
+  run("v6 c++ barriers, sgpr tw", k_bfly<6, false>, d, tw, q);
+  run("v6 c++ barriers, lane tw", k_bfly<6, true>, d, tw, q);
   return 0;
 }
