@@ -418,7 +418,9 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
   __shared__ u64 lds[G::LDS_R];
   u32 l, rest;
   xcd_limb_split(blockIdx.x, nlimbs, l, rest);
-  const u32 tile = rest % G::TILES_R, p = rest / G::TILES_R;
+  // poly fastest: consecutive workgroups of one XCD reuse a row's twiddles while they are hot
+  const u32 polys = gridDim.x / (nlimbs * G::TILES_R);
+  const u32 p = rest % polys, tile = rest / polys;
   const u32 limb = limb0 + l;
   const u32 t = threadIdx.x % G::TPS_R, sub = threadIdx.x / G::TPS_R;
   const u32 row = tile * G::SUBS_R + sub;
@@ -470,7 +472,9 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   __shared__ u64 lds[H::ROWS * H::ROWW];
   u32 l, rest;
   xcd_limb_split(blockIdx.x, nlimbs, l, rest);
-  const u32 tile = rest % H::TILES, b = rest / H::TILES;
+  // ciphertext fastest: consecutive workgroups of one XCD reuse a row's twiddles while hot
+  const u32 batch = gridDim.x / (nlimbs * H::TILES);
+  const u32 b = rest % batch, tile = rest / batch;
   const u32 limb = limb0 + l;
   const ModParams m = mods[limb];
   const u64 q = m.q;
