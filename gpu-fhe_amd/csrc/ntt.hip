@@ -16,7 +16,7 @@
 // table psi^brv (16-byte {w, floor(w 2^64 / q)} Shoup pairs, L2-resident).  Butterflies are
 // Harvey-lazy: forward values live in [0, 4q), inverse in [0, 2q); the last pass reduces to [0, q).
 //
-// HomMult (config 3) = 3 launches: column-forward on the 4 input polys -> one fused row kernel
+// HomMult (config 3) = 4 launches: column-forward on a, then on b -> one fused row kernel
 // (row-forward x4, tensor d0 = A0B0, d1 = A0B1 + A1B0, d2 = A1B1 in LDS, row-inverse x3) ->
 // column-inverse on the 3 output polys.
 #include <type_traits>
