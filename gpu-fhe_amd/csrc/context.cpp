@@ -130,6 +130,11 @@ ModParams make_mod_params(u64 q) {
   m.sh_a = bl - 1;
   m.sh_b = bl + 3;
   m.mu = (u64)(((u128)1 << (2 * bl + 2)) / q);
+  if (q & 1) {
+    u64 inv = q;  // Newton: each step doubles the correct low bits (q * q = 1 mod 8)
+    for (int i = 0; i < 5; ++i) inv *= 2 - q * inv;
+    m.qinv = 0 - inv;
+  }
   return m;
 }
 
@@ -195,8 +200,11 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
   }
   FHE_HIP_CHECK(hipSetDevice(device));
 
+  int cus = 0;
+  FHE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   auto* c = new fhe_ctx();
   c->device = device;
+  c->num_cus = cus;
   c->log_n = log_n;
   c->n = n;
   c->L = L;
@@ -205,7 +213,7 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
   c->alpha = K ? (L + dnum - 1) / dnum : 0;
   c->moduli = mods;
   const size_t M = mods.size();
-  std::vector<ulonglong2> twf(M * n), twi(M * n), nfold(2 * M);
+  std::vector<ulonglong2> twf(M * n), twi(M * n), nfold(4 * M);
   c->psi.resize(M);
   c->mods_host.resize(M);
   std::vector<u64> pw(n), pwi(n);
@@ -225,14 +233,18 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
       twi[i * n + k] = shoup_pair(pwi[b], m);
     }
     const u64 n_inv = powmod_u64(n % m, m - 2, m);
-    nfold[2 * i] = shoup_pair(n_inv, m);
-    nfold[2 * i + 1] = shoup_pair(mulmod_u64(twi[i * n + 1].x, n_inv, m), m);
+    const u64 r_mod = (u64)(((u128)1 << 64) % m);  // Montgomery R = 2^64 mod q
+    const u64 nf1 = mulmod_u64(twi[i * n + 1].x, n_inv, m);
+    nfold[4 * i] = shoup_pair(n_inv, m);
+    nfold[4 * i + 1] = shoup_pair(nf1, m);
+    nfold[4 * i + 2] = shoup_pair(mulmod_u64(n_inv, r_mod, m), m);  // HomMult: undo R^-1
+    nfold[4 * i + 3] = shoup_pair(mulmod_u64(nf1, r_mod, m), m);
   }
   int rc = kOk;
   if ((rc = upload(&c->d_mods, c->mods_host.data(), M)) ||
       (rc = upload(&c->d_tw_fwd, twf.data(), M * n)) ||
       (rc = upload(&c->d_tw_inv, twi.data(), M * n)) ||
-      (rc = upload(&c->d_nfold, nfold.data(), 2 * M)) || (rc = build_rns_tables(c))) {
+      (rc = upload(&c->d_nfold, nfold.data(), 4 * M)) || (rc = build_rns_tables(c))) {
     ctx_destroy(c);
     return rc;
   }

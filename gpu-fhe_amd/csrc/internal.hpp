@@ -29,6 +29,7 @@ void prof_mark(hipStream_t s, const char* name);
 // Immutable after fhe_ctx_create, except for the lazily grown internal workspace.
 struct fhe_ctx {
   int device = 0;
+  int num_cus = 0;  // compute units of `device` (one-generation grids of the item-loop kernels)
   uint32_t log_n = 0;
   uint64_t n = 0;
   uint32_t L = 0, K = 0, dnum = 0, alpha = 0;
@@ -39,7 +40,9 @@ struct fhe_ctx {
   fhe::ModParams* d_mods = nullptr;  // [L + K]
   ulonglong2* d_tw_fwd = nullptr;    // [L + K][N] (psi^brv(k), Shoup)
   ulonglong2* d_tw_inv = nullptr;    // [L + K][N] (psi^-brv(k), Shoup)
-  ulonglong2* d_nfold = nullptr;     // [L + K][2] (N^-1, psi^-1 N^-1) with Shoup
+  // [L + K][4] Shoup pairs: N^-1, psi^-1 N^-1 (last inverse stage), and the same times
+  // R = 2^64 (HomMult's inverse, undoing the Montgomery tensor's R^-1)
+  ulonglong2* d_nfold = nullptr;
 
   // Hybrid key-switch base-conversion constants (rns.hip), Shoup pairs, device resident.
   // Digit j covers Q-limbs [j * alpha, min(L, (j + 1) * alpha)).

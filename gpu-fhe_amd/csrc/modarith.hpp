@@ -2,7 +2,8 @@
 //
 // Replaces the reference's numpy `%` (/root/reference/arithmetic.py:5,9,13) with exact
 // word-level reductions.  gfx950 has no 64x64->128 multiply: a 64-bit product is built from
-// v_mad_u64_u32 / v_mul_hi_u32 / v_mul_lo_u32, all ~quarter-rate (profiles/r01_imul_rate.txt),
+// v_mad_u64_u32 / v_mul_hi_u32 / v_mul_lo_u32, ~1.8x the issue cost of a 32-bit add
+// (tools/microbench/isa_rate.hip, profiles/r01_isa_rate.txt),
 // so every routine here is written to minimise the number of 32x32 partial products.
 //
 // Conventions (shared with oracle/fhe_oracle.c):
@@ -27,6 +28,7 @@ struct ModParams {
   u64 mu;    // Barrett: floor(2^(2 bitlen + 2) / q)
   u32 sh_a;  // bitlen - 1
   u32 sh_b;  // bitlen + 3  (= b - a)
+  u64 qinv;  // Montgomery (R = 2^64): -q^-1 mod 2^64 for odd q, else 0
 };
 
 __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return (u64)(((u128)a * b) >> 64); }
@@ -87,6 +89,32 @@ __device__ __forceinline__ u64 shoup_fast(u64 y, u64 w, u64 ws, u64 nq) {
   return ((u64)(u32)c << 32) | (u32)t;
 }
 
+// y * w mod q up to two q, any y < 2^64, result in [0, 3q): Shoup with the quotient estimated
+// from three of the four partial products of y * w'.  Dropping hi(y0 s0) (< 2^32 in the 2^32
+// column) lowers h = floor(y w' / 2^64) by at most 1, so r = y w - h q grows by at most q; the
+// 2^32-column sum y1 s0 + y0 s1 may carry into bit 64, which is added back into the high mad.
+// Quotient: 3 mads + 1 select (vs 1 mul_hi + 3 mads + a 64-bit add for the exact one).
+// Remainder: lo64(y w + h nq), nq = -q mod 2^64 (exact: the true value is < 3q).
+__device__ __forceinline__ u64 shoup_q3(u64 y, u64 w, u64 ws, u64 nq) {
+  const u32 y0 = (u32)y, y1 = (u32)(y >> 32);
+  const u32 s0 = (u32)ws, s1 = (u32)(ws >> 32);
+  const u64 a = (u64)y1 * s0;
+  u64 b;
+  u64 cmask;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(b), "=s"(cmask) : "v"(y0), "v"(s1), "v"(a));
+  u32 c;
+  asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(c) : "s"(cmask));
+  const u64 h = mad_u64_u32(y1, s1, ((u64)c << 32) | (u32)(b >> 32));
+  // lo64(y w + h nq): the two low-word products as chained mads, the four cross terms only
+  // contribute their low words to the high word (2 mads + 4 mul_lo, no 64-bit add or borrow)
+  const u32 w0 = (u32)w, w1 = (u32)(w >> 32), n0 = (u32)nq, n1 = (u32)(nq >> 32);
+  const u32 h0 = (u32)h, h1 = (u32)(h >> 32);
+  u64 t = mad_u64_u32(h0, n0, (u64)y0 * w0);
+  FHE_OPAQUE(t);
+  const u32 hi = (u32)(t >> 32) + y1 * w0 + y0 * w1 + h1 * n0 + h0 * n1;
+  return ((u64)hi << 32) | (u32)t;
+}
+
 // a - b + k for a + k > b, with kp1 = k + 1: a + k + 1 + ~b, two 64-bit adds, no borrow chain.
 __device__ __forceinline__ u64 sub_plus(u64 a, u64 b, u64 kp1) {
   u64 nb = ~b;
@@ -105,6 +133,15 @@ __device__ __forceinline__ u64 barrett_reduce(u128 z, const ModParams& m) {
 
 __device__ __forceinline__ u64 mulmod_barrett(u64 a, u64 b, const ModParams& m) {
   return barrett_reduce((u128)a * b, m);
+}
+
+// Montgomery reduction with R = 2^64 of t = (thi, tlo) < q 2^64: returns t R^-1 mod q up to one
+// q, in [0, 2q).  m = tlo qinv (qinv = -q^-1) makes t + m q a multiple of 2^64, whose low word
+// therefore carries out exactly when tlo != 0.  No shifts or compares on the modulus, unlike
+// Barrett with its per-modulus shift counts.
+__device__ __forceinline__ u64 mont_reduce_lazy(u64 tlo, u64 thi, u64 q, u64 qinv) {
+  const u64 m = tlo * qinv;
+  return thi + mulhi64(m, q) + (tlo != 0 ? 1 : 0);
 }
 
 // Full reduction of any 64-bit x into [0, q), any q >= 2: Barrett for 2^31 <= q < 2^61

@@ -14,11 +14,15 @@
 // Inside a pass, each thread holds E = 16 elements of one sub-transform in VGPRs and runs up to
 // 4 butterfly stages per LDS round trip (radix-16 rounds); twiddles come from the per-limb
 // table psi^brv (16-byte {w, floor(w 2^64 / q)} Shoup pairs, L2-resident).  Butterflies are
-// Harvey-lazy: forward values live in [0, 4q), inverse in [0, 2q); the last pass reduces to [0, q).
+// lazy (FHE_BFLY below): forward values live in [0, 8q), inverse in [0, 3q) between stages and
+// passes; the last pass reduces to [0, q).
 //
 // HomMult (config 3) = 4 launches: column-forward on a, then on b -> one fused row kernel
 // (row-forward x4, tensor d0 = A0B0, d1 = A0B1 + A1B0, d2 = A1B1 in LDS, row-inverse x3) ->
 // column-inverse on the 3 output polys.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -36,16 +40,20 @@ constexpr int kElog = FHE_ELOG;
 constexpr int kE = 1 << kElog;
 constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per workgroup
 // FHE_NTT_ABLATE (timing-only A/B builds, tools/build_variant.sh; never the shipped library):
-// 1 = skip the butterflies of the generic passes, 2 = skip their global loads/stores.
+// 1 = skip the butterflies of the generic passes, 2 = skip their global loads/stores,
+// 3 = row passes read row 0's twiddles for every row (wrong results; twiddle-fetch cost).
 #ifndef FHE_NTT_ABLATE
 #define FHE_NTT_ABLATE 0
 #endif
-// FHE_BFLY_ASM: butterflies through the instruction-shaped helpers of modarith.hpp (1) or the
-// plain C++ Shoup (0).  Shaped wins 20 % in the register-only microbenchmark
-// (tools/microbench/bfly_rate.hip) but ties inside the kernels, where register-pair moves for the
-// mad addends eat the saved instructions (tools/isa_cost.py: 2860 vs 2937 units per column pass).
-#ifndef FHE_BFLY_ASM
-#define FHE_BFLY_ASM 0
+// FHE_BFLY selects the butterfly arithmetic:
+//  0  Harvey with exact Shoup (forward values in [0, 4q), inverse in [0, 2q));
+//  1  the same through the instruction-shaped helpers of modarith.hpp (wins 20 % in the
+//     register-only microbenchmark tools/microbench/bfly_rate.hip, ties inside the kernels);
+//  2  Shoup with the 3-product quotient estimate (shoup_q3, products in [0, 3q)) and wider lazy
+//     ranges: forward values in [0, 8q) (u = x mod 4q, outputs u + t and u - t + 3q), inverse in
+//     [0, 3q) (sum mod 3q, (u - v + 3q) w).  Needs 8q < 2^64, i.e. q < 2^61 (ctx_create checks).
+#ifndef FHE_BFLY
+#define FHE_BFLY 2
 #endif
 #ifndef FHE_HM_POLY_MAJOR
 #define FHE_HM_POLY_MAJOR 1
@@ -56,8 +64,19 @@ constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per work
 #ifndef FHE_NTT_MAX_WAVES
 #define FHE_NTT_MAX_WAVES 8
 #endif
+// ... and the occupancy they must keep: LDS allows 4 workgroups (16 waves) per CU, so anything
+// above 128 VGPRs would cost waves; the item loops' prefetch registers must fit under that.
+#ifndef FHE_NTT_MIN_WAVES
+#define FHE_NTT_MIN_WAVES 4
+#endif
+// FHE_ITEM_LOOP bit 0: column passes, bit 1: row passes run one-generation grids whose
+// workgroups loop over items, prefetching the next one (else one workgroup per item).
+#ifndef FHE_ITEM_LOOP
+#define FHE_ITEM_LOOP 0
+#endif
+constexpr bool kLoopCol = (FHE_ITEM_LOOP & 1) != 0, kLoopRow = (FHE_ITEM_LOOP & 2) != 0;
 #define FHE_KATTR \
-  __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, FHE_NTT_MAX_WAVES)))
+  __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES)))
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -170,18 +189,85 @@ struct PolyMap {
 };
 static inline PolyMap flat_map(u64 pstride) { return PolyMap{1, pstride, 0, pstride, 0}; }
 
+// The distinct twiddles of one round: butterfly (stage b, pair j) uses twiddle group
+// g = (tp | jpos(j)) >> (LO + b + 1); slot[b][j] numbers the distinct (b, g - tp part) pairs and
+// rep[] keeps one representative j per slot.
+template <int LOGR, int KB, int LO>
+struct TwSlots {
+  using Lay = Layout<LOGR, KB, LO>;
+  struct Tab {
+    int ns = 0;
+    int slot[kElog][kE] = {};
+    int rep_b[kElog * kE] = {}, rep_j[kElog * kE] = {};
+  };
+  static constexpr Tab make() {
+    Tab t{};
+    for (int b = 0; b < KB; ++b)
+      for (int j = 0; j < kE; ++j) {
+        if (j & (1 << b)) continue;
+        const u32 key = Lay::jpos(j) >> (LO + b + 1);
+        int found = -1;
+        for (int s = 0; s < t.ns; ++s)
+          if (t.rep_b[s] == b && (Lay::jpos(t.rep_j[s]) >> (LO + b + 1)) == key) found = s;
+        if (found < 0) {
+          found = t.ns++;
+          t.rep_b[found] = b;
+          t.rep_j[found] = j;
+        }
+        t.slot[b][j] = found;
+      }
+    return t;
+  }
+  static constexpr Tab T = make();
+};
+
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
 // Runs one round's butterfly stages on the 16 values a thread holds in registers.
 // Element j sits at sub-transform position tp | Lay::jpos(j).  `base` selects the twiddle rows:
 // local stage st, group g reads tw[(base << st) + g] (base = 1 for the column pass, R1 + row for
-// the row pass).
-template <int LOGR, int KB, int LO, bool FWD, int FIN>
+// the row pass).  All of the round's twiddle loads are issued first; then `hook` runs (after a
+// compiler memory fence, so its global loads queue behind the twiddles and waiting for a twiddle
+// never waits for them: vmcnt retires in issue order).
+// GATHER = false leaves the twiddle loads to the scheduler, next to their butterflies (better for
+// the column pass, whose twiddles are few and shared); true issues them all first (the row passes:
+// per-lane twiddles from L2, whose latency then overlaps instead of stalling each stage).
+template <int LOGR, int KB, int LO, bool FWD, int FIN, bool GATHER = false, class Hook = NoHook>
 __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
                                               const ulonglong2* __restrict__ tw, const u32 base,
                                               const u64 q, const ulonglong2 nf0,
-                                              const ulonglong2 nf1) {
+                                              const ulonglong2 nf1, const Hook& hook = Hook{}) {
   using Lay = Layout<LOGR, KB, LO>;
+  using TS = TwSlots<LOGR, KB, LO>;
   constexpr int E = Lay::E;
-  const u64 q2 = 2 * q, nq = 0 - q, nq2 = 0 - q2, q2p1 = q2 + 1;
+  ulonglong2 tws[GATHER && TS::T.ns > 0 ? TS::T.ns : 1];
+  if constexpr (GATHER) {
+    static_for<0, TS::T.ns>([&](auto sc) {
+      constexpr int sl = decltype(sc)::value;
+      constexpr int b = TS::T.rep_b[sl];
+      constexpr int bitpos = LO + b;
+      constexpr int st = LOGR - 1 - bitpos;
+      if constexpr (!(FIN == kFinalInv && st == 0)) {  // the last inverse stage folds N^-1 instead
+        const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(TS::T.rep_j[sl]) >> (bitpos + 1));
+        tws[sl] = tw[(base << st) + g];
+      }
+    });
+    asm volatile("" ::: "memory");
+  }
+  hook();
+  auto twiddle = [&](int b, int j, int bitpos, int st) {
+    if constexpr (GATHER) return tws[TS::T.slot[b][j]];
+    const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(j) >> (bitpos + 1));
+    return tw[(base << st) + g];
+  };
+  const u64 q2 = 2 * q, nq = 0 - q;
+  [[maybe_unused]] const u64 nq2 = 0 - q2, q2p1 = q2 + 1;
+  // 3q as an opaque uniform: otherwise u + 3q is strength-reduced into a mad per butterfly
+  [[maybe_unused]] u64 q3 = 3 * q;
+  [[maybe_unused]] const u64 q4 = 4 * q;
+  asm("" : "+s"(q3));
   if constexpr (FWD) {
 #pragma unroll
     for (int b = KB - 1; b >= 0; --b) {
@@ -191,15 +277,20 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       for (int j = 0; j < E; ++j) {
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
-        const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(j) >> (bitpos + 1));
-        const ulonglong2 w = tw[(base << st) + g];
-        // Harvey CT: u in [0, 4q) -> [0, 2q); v = w x[jj] in [0, 2q); outputs in [0, 4q)
-#if FHE_BFLY_ASM
+        const ulonglong2 w = twiddle(b, j, bitpos, st);
+#if FHE_BFLY == 2
+        // CT: x in [0, 8q): u = x mod 4q in [0, 4q); v = w x[jj] in [0, 3q); outputs in [0, 7q)
+        const u64 u = csub(x[j], q4);
+        const u64 v = shoup_q3(x[jj], w.x, w.y, nq);
+        x[j] = u + v;
+        x[jj] = u - v + q3;
+#elif FHE_BFLY == 1
         const u64 u = csub_fast(x[j], nq2);
         const u64 v = shoup_fast(x[jj], w.x, w.y, nq);
         x[j] = u + v;
         x[jj] = sub_plus(u, v, q2p1);
 #else
+        // Harvey CT: u in [0, 4q) -> [0, 2q); v = w x[jj] in [0, 2q); outputs in [0, 4q)
         const u64 u = csub(x[j], q2);
         const u64 v = shoup_lazy(x[jj], w.x, w.y, q);
         x[j] = u + v;
@@ -209,7 +300,13 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
     }
     if constexpr (FIN == kFinalFwd) {
 #pragma unroll
-      for (int j = 0; j < E; ++j) x[j] = csub(csub(x[j], q2), q);
+      for (int j = 0; j < E; ++j) {
+#if FHE_BFLY == 2
+        x[j] = csub(csub(csub(x[j], q4), q2), q);
+#else
+        x[j] = csub(csub(x[j], q2), q);
+#endif
+      }
     }
   } else {
 #pragma unroll
@@ -220,21 +317,31 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       for (int j = 0; j < E; ++j) {
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
-        // Harvey GS: inputs in [0, 2q); sum -> [0, 2q); (u - v + 2q) w -> [0, 2q)
         const u64 u = x[j], v = x[jj];
-#if FHE_BFLY_ASM
+#if FHE_BFLY == 2
+        // GS: inputs in [0, 3q); sum -> [0, 3q); (u - v + 3q) w -> [0, 3q)
+        const u64 sum = u + v, dif = u - v + q3;
+#elif FHE_BFLY == 1
         const u64 sum = u + v, dif = sub_plus(u, v, q2p1);
 #else
+        // Harvey GS: inputs in [0, 2q); sum -> [0, 2q); (u - v + 2q) w -> [0, 2q)
         const u64 sum = u + v, dif = u - v + q2;
 #endif
         if (FIN == kFinalInv && st == 0) {
           // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
+#if FHE_BFLY == 2
+          x[j] = csub(csub(shoup_q3(sum, nf0.x, nf0.y, nq), q2), q);
+          x[jj] = csub(csub(shoup_q3(dif, nf1.x, nf1.y, nq), q2), q);
+#else
           x[j] = csub(shoup_lazy(sum, nf0.x, nf0.y, q), q);
           x[jj] = csub(shoup_lazy(dif, nf1.x, nf1.y, q), q);
+#endif
         } else {
-          const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(j) >> (bitpos + 1));
-          const ulonglong2 w = tw[(base << st) + g];
-#if FHE_BFLY_ASM
+          const ulonglong2 w = twiddle(b, j, bitpos, st);
+#if FHE_BFLY == 2
+          x[j] = csub(sum, q3);
+          x[jj] = shoup_q3(dif, w.x, w.y, nq);
+#elif FHE_BFLY == 1
           x[j] = csub_fast(sum, nq2);
           x[jj] = shoup_fast(dif, w.x, w.y, nq);
 #else
@@ -257,13 +364,18 @@ constexpr bool contiguous16() {
 
 // Global-memory views of one sub-transform.  Column pass: position p at base[p * R2] (lanes run
 // over adjacent columns, so every access is coalesced).  Row pass: position p at base[p].
+// `base` is wave-uniform and `lane` the per-lane element offset, so every access is an SGPR base
+// (the position's constant part folded in by the scalar unit) plus one 32-bit VGPR offset: no
+// per-element 64-bit address registers.
 template <int STRIDE>
 struct GView {
   u64* base;
+  u32 lane;
   template <class Lay>
   __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
+    const u32 off = lane + tp * STRIDE;
     if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
-      const ulonglong2* v = reinterpret_cast<const ulonglong2*>(base + tp);
+      const ulonglong2* v = reinterpret_cast<const ulonglong2*>(base + off);
 #pragma unroll
       for (int j = 0; j < kE / 2; ++j) {
         const ulonglong2 w = v[j];
@@ -272,18 +384,19 @@ struct GView {
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) x[j] = base[(u64)(tp | Lay::jpos(j)) * STRIDE];
+      for (int j = 0; j < kE; ++j) x[j] = (base + (u64)Lay::jpos(j) * STRIDE)[off];
     }
   }
   template <class Lay>
   __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
+    const u32 off = lane + tp * STRIDE;
     if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
-      ulonglong2* v = reinterpret_cast<ulonglong2*>(base + tp);
+      ulonglong2* v = reinterpret_cast<ulonglong2*>(base + off);
 #pragma unroll
       for (int j = 0; j < kE / 2; ++j) v[j] = make_ulonglong2(x[2 * j], x[2 * j + 1]);
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) base[(u64)(tp | Lay::jpos(j)) * STRIDE] = x[j];
+      for (int j = 0; j < kE; ++j) (base + (u64)Lay::jpos(j) * STRIDE)[off] = x[j];
     }
   }
 };
@@ -305,15 +418,32 @@ struct LView {
   }
 };
 
-// A whole 2^LOGR-point pass for one sub-transform: round 0 loads straight from global memory,
-// rounds exchange through LDS, the last round stores straight to global memory.  Every thread
-// of the workgroup must call this (it contains barriers); `active` masks the arithmetic/IO.
-template <int LOGR, bool FWD, int FIN, int SYNC, class GIn, class GOut, class LV>
-__device__ __forceinline__ void ntt_pass(const GIn& gin, const GOut& gout, const LV& lv, u32 t,
-                                         bool active, const ulonglong2* __restrict__ tw, u32 base,
-                                         u64 q, ulonglong2 nf0, ulonglong2 nf1) {
+// Round-0 global load of one sub-transform into registers (issued ahead of the work that needs
+// it: the kernels below prefetch their next item while computing the current one).
+template <int LOGR, bool FWD, class GIn>
+__device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
   using Rd = Rounds<LOGR>;
-  u64 x[kE];
+  using Lay = Layout<LOGR, FWD ? Rd::kb(0) : Rd::kb_inv(0), FWD ? Rd::lo_fwd(0) : Rd::lo_inv(0)>;
+#if FHE_NTT_ABLATE == 2  // timing-only build: no global loads (synthetic values below q)
+  (void)gin;
+  for (int j = 0; j < kE; ++j) x[j] = ((u64)(Lay::tpos(t) + j) * 0x9e3779b97f4a7c15ull) >> 5;
+#else
+  gin.template load<Lay>(x, Lay::tpos(t));
+#endif
+}
+
+// The rest of a 2^LOGR-point pass on values pass_load brought in: rounds exchange through LDS,
+// the last round stores straight to global memory.  Every thread of the LDS-sharing group must
+// call it (it contains the exchange fences; the first one also orders this item's LDS writes
+// after the previous item's LDS reads).
+// `hook` runs once round 0's twiddle loads are in flight (the item loops' prefetch).
+template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, bool LOOPED, class GOut, class LV,
+          class Hook = NoHook>
+__device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const LV& lv, u32 t,
+                                         const ulonglong2* __restrict__ tw, u32 base, u64 q,
+                                         ulonglong2 nf0, ulonglong2 nf1,
+                                         const Hook& hook = Hook{}) {
+  using Rd = Rounds<LOGR>;
   static_for<0, Rd::NR>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int KB = FWD ? Rd::kb(k) : Rd::kb_inv(k);
@@ -321,35 +451,35 @@ __device__ __forceinline__ void ntt_pass(const GIn& gin, const GOut& gout, const
     constexpr int F = (k == Rd::NR - 1) ? FIN : kNotFinal;
     using Lay = Layout<LOGR, KB, LO>;
     const u32 tp = Lay::tpos(t);
-    if constexpr (k == 0) {
-#if FHE_NTT_ABLATE == 2  // timing-only build: no global loads (synthetic values)
-      if (active)
-        for (int j = 0; j < kE; ++j) x[j] = (u64)(tp + j) * 0x9e3779b97f4a7c15ull % q;
-#else
-      if (active) gin.template load<Lay>(x, tp);
-#endif
-    } else {
+    if constexpr (k > 0) {
       lds_sync<SYNC>();
-      if (active) lv.template load<Lay>(x, tp);
+      lv.template load<Lay>(x, tp);
     }
 #if FHE_NTT_ABLATE == 1  // timing-only build: no butterflies
     for (int j = 0; j < kE; ++j) asm volatile("" : "+v"(x[j]));
 #else
-    if (active) round_compute<LOGR, KB, LO, FWD, F>(x, tp, tw, base, q, nf0, nf1);
+    // an opaque twiddle base per round keeps the scheduler from hoisting every round's twiddle
+    // loads to the top (the gathered row passes, item loops: their VGPRs would cost occupancy or
+    // spill); the column pass's few shared twiddles are left to the scheduler
+    const ulonglong2* twk = tw;
+    if constexpr (LOOPED || GATHER) asm volatile("" : "+s"(twk));
+    if constexpr (k == 0)
+      round_compute<LOGR, KB, LO, FWD, F, GATHER>(x, tp, twk, base, q, nf0, nf1, hook);
+    else
+      round_compute<LOGR, KB, LO, FWD, F, GATHER>(x, tp, twk, base, q, nf0, nf1);
 #endif
     if constexpr (k == Rd::NR - 1) {
 #if FHE_NTT_ABLATE == 2
-      if (active) {
-        u64 acc = 0;
-        for (int j = 0; j < kE; ++j) acc ^= x[j];
-        if (acc == 0x5a5a5a5a5a5a5a5aull) gout.template store<Lay>(x, tp);  // practically never
-      }
+      u64 acc = 0;
+      for (int j = 0; j < kE; ++j) acc ^= x[j];
+      if (acc == 0x5a5a5a5a5a5a5a5aull) gout.template store<Lay>(x, tp);  // practically never
 #else
-      if (active) gout.template store<Lay>(x, tp);
+      gout.template store<Lay>(x, tp);
 #endif
     } else {
-      if (k > 0) lds_sync<SYNC>();
-      if (active) lv.template store<Lay>(x, tp);
+      // round 0's store needs a fence only when the previous item's last LDS reads precede it
+      if (k > 0 || LOOPED) lds_sync<SYNC>();
+      lv.template store<Lay>(x, tp);
     }
   });
 }
@@ -375,64 +505,117 @@ struct Geo {
   static_assert(N1 >= kElog - 1 && N2 >= kElog, "log N too small for this kernel family");
 };
 
-// Column pass. src/dst: [polys][nlimbs][N] via PolyMap; grid = polys * nlimbs * TILES_C.
+// Item loops.  A pass kernel runs a one-generation grid (tools: launch_items) and each
+// workgroup walks items b, b + grid, b + 2 grid, ...; the next item's round-0 loads are issued
+// before the current item's butterflies, so HBM latency hides behind compute instead of
+// needing more resident waves (LDS caps these kernels at 4 workgroups per CU).  grid is a
+// multiple of 8, so an item keeps the XCD (blockIdx % 8) its index maps to.
+
+// Column pass over items (p, l, tile) of src/dst [polys][nlimbs][N] via PolyMap.
 template <int LOGN, bool FWD>
 __global__ FHE_KATTR void k_ntt_col(const u64* __restrict__ src,
                                                       u64* __restrict__ dst, u32 nlimbs,
-                                                      u32 limb0, PolyMap pm,
+                                                      u32 limb0, PolyMap pm, u32 items,
                                                       const ulonglong2* __restrict__ tw_all,
                                                       const ulonglong2* __restrict__ nfold,
                                                       const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[G::LDS_C];
-  const u32 tile = blockIdx.x % G::TILES_C;
-  const u32 pl = blockIdx.x / G::TILES_C;
-  const u32 l = pl % nlimbs, p = pl / nlimbs;
-  const u32 limb = limb0 + l;
-  const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
-  const u64 q = mods[limb].q;
-  const ulonglong2* tw = tw_all + (u64)limb * N;
   const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
-  ulonglong2 nf0 = {0, 0}, nf1 = {0, 0};
-  if (!FWD) {
-    nf0 = nfold[2 * limb];
-    nf1 = nfold[2 * limb + 1];
-  }
-  const GView<G::R2> gin{const_cast<u64*>(src) + pm.src(p) + loc + sub};
-  const GView<G::R2> gout{dst + pm.dst(p) + loc + sub};
   const LView<G::CS, false> lv{lds + sub};
-  ntt_pass<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync>(gin, gout, lv, t, true, tw, 1u, q,
-                                                               nf0, nf1);
+  struct Item {  // all wave-uniform
+    u32 limb;
+    u64 src, dst;
+  };
+  auto decode = [&](u32 it) {
+    const u32 tile = it % G::TILES_C, pl = it / G::TILES_C;
+    const u32 l = pl % nlimbs, p = pl / nlimbs;
+    const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
+    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), pm.src(p) + loc, pm.dst(p) + loc};
+  };
+  u32 it = blockIdx.x;
+  if (it >= items) return;
+  Item cur = decode(it);
+  u64 x[kE], y[kE];
+  pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(src) + cur.src, sub}, t, x);
+  while (true) {
+    const u32 nx = it + gridDim.x;
+    const bool more = kLoopCol && nx < items;
+    const Item nxt = more ? decode(nx) : cur;
+    auto prefetch = [&] {
+      if (more) pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(src) + nxt.src, sub}, t, y);
+    };
+    ulonglong2 nf0 = {0, 0}, nf1 = {0, 0};
+    if (!FWD) {
+      nf0 = nfold[4 * cur.limb];
+      nf1 = nfold[4 * cur.limb + 1];
+    }
+    pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol>(
+        x, GView<G::R2>{dst + cur.dst, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
+        nf0, nf1, prefetch);
+    if (!more) break;
+    it = nx;
+    cur = nxt;
+#pragma unroll
+    for (int j = 0; j < kE; ++j) x[j] = y[j];
+  }
 }
 
-// Row pass. grid = polys * nlimbs * TILES_R.
+// Row pass over items (l, p, tile): the limb follows the XCD and the poly varies fastest, so the
+// workgroups of one XCD reuse a row's twiddles while they are hot.
 template <int LOGN, bool FWD>
 __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
                                                       u64* __restrict__ dst, u32 nlimbs,
-                                                      u32 limb0, PolyMap pm,
+                                                      u32 limb0, PolyMap pm, u32 items,
                                                       const ulonglong2* __restrict__ tw_all,
                                                       const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[G::LDS_R];
-  u32 l, rest;
-  xcd_limb_split(blockIdx.x, nlimbs, l, rest);
-  // poly fastest: consecutive workgroups of one XCD reuse a row's twiddles while they are hot
-  const u32 polys = gridDim.x / (nlimbs * G::TILES_R);
-  const u32 p = rest % polys, tile = rest / polys;
-  const u32 limb = limb0 + l;
-  const u32 t = threadIdx.x % G::TPS_R, sub = threadIdx.x / G::TPS_R;
-  const u32 row = tile * G::SUBS_R + sub;
-  const u64 loc = (u64)l * N + (u64)row * G::R2;
-  const u64 q = mods[limb].q;
-  const ulonglong2* tw = tw_all + (u64)limb * N;
-  const GView<1> gin{const_cast<u64*>(src) + pm.src(p) + loc};
-  const GView<1> gout{dst + pm.dst(p) + loc};
-  const LView<1, true> lv{lds + sub * G::RS};
   static_assert(64 % G::TPS_R == 0, "a row must not straddle wavefronts");
-  ntt_pass<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync>(gin, gout, lv, t, true, tw,
-                                                               (u32)G::R1 + row, q, {0, 0}, {0, 0});
+  const u32 t = threadIdx.x % G::TPS_R, sub = threadIdx.x / G::TPS_R;
+  const LView<1, true> lv{lds + sub * G::RS};
+  const u32 polys = items / (nlimbs * G::TILES_R);
+  struct Item {  // all wave-uniform; this lane's row is row0 + sub
+    u32 limb, row0;
+    u64 src, dst;
+  };
+  auto decode = [&](u32 it) {
+    u32 l, rest;
+    xcd_limb_split(it, nlimbs, l, rest);
+    const u32 p = rest % polys, tile = rest / polys;
+    const u32 row0 = tile * G::SUBS_R;
+    const u64 loc = (u64)l * N + (u64)row0 * G::R2;
+    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), row0, pm.src(p) + loc, pm.dst(p) + loc};
+  };
+  const u32 lane = sub * G::R2;
+  u32 it = blockIdx.x;
+  if (it >= items) return;
+  Item cur = decode(it);
+  u64 x[kE], y[kE];
+  pass_load<G::N2, FWD>(GView<1>{const_cast<u64*>(src) + cur.src, lane}, t, x);
+  while (true) {
+    const u32 nx = it + gridDim.x;
+    const bool more = kLoopRow && nx < items;
+    const Item nxt = more ? decode(nx) : cur;
+    auto prefetch = [&] {
+      if (more) pass_load<G::N2, FWD>(GView<1>{const_cast<u64*>(src) + nxt.src, lane}, t, y);
+    };
+    pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, kLoopRow>(
+        x, GView<1>{dst + cur.dst, lane}, lv, t, tw_all + (u64)cur.limb * N,
+#if FHE_NTT_ABLATE == 3  // timing-only build: every row uses row 0's twiddles (cache-resident)
+        (u32)G::R1,
+#else
+        (u32)G::R1 + cur.row0 + sub,
+#endif
+        mods[cur.limb].q, {0, 0}, {0, 0}, prefetch);
+    if (!more) break;
+    it = nx;
+    cur = nxt;
+#pragma unroll
+    for (int j = 0; j < kE; ++j) x[j] = y[j];
+  }
 }
 
 // Fused HomMult row kernel: rows of the 4 column-transformed inputs (layout [batch][4][nlimbs][N]
@@ -453,9 +636,11 @@ struct HmGeo {
   // FHE_HM_POLY_MAJOR: thread group g = one polynomial spread over whole wavefronts, so during the
   // 3-poly inverse the 4th group is a whole idle wave (its SIMD slots go to other waves) instead
   // of idle lanes inside every wave (measured: VALUBusy ~100 % with 77 % lane utilisation).
-  // Exchanges then cross waves and need the block barrier.
+  // A polynomial's rows then sit in one wavefront, so its round exchanges stay wave-local and
+  // only the tensor (reading all four slots) needs the block barrier.
   static constexpr bool POLY_MAJOR = FHE_HM_POLY_MAJOR != 0;
-  static constexpr int SYNC = (!POLY_MAJOR && LANES_ROW <= 64) ? kWaveSync : kBlockSync;
+  static constexpr int SYNC_TENSOR = (!POLY_MAJOR && LANES_ROW <= 64) ? kWaveSync : kBlockSync;
+  static constexpr int SYNC_ROUND = (POLY_MAJOR || LANES_ROW <= 64) ? kWaveSync : kBlockSync;
 };
 
 template <int LOGN>
@@ -481,7 +666,9 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   const u64 limbN = (u64)nlimbs * N;
   u32 sub, grp, t;
   if constexpr (H::POLY_MAJOR) {  // [poly][row][lane]
-    grp = threadIdx.x / (H::ROWS * H::TPS);
+    // rotate which wave gets which poly per workgroup: the wave that idles through the 3-poly
+    // inverse must not land on the same SIMD in every workgroup
+    grp = (threadIdx.x / (H::ROWS * H::TPS) + blockIdx.x) % 4;
     sub = (threadIdx.x / H::TPS) % H::ROWS;
     t = threadIdx.x % H::TPS;
   } else {  // [row][poly][lane]
@@ -496,7 +683,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   const u32 base = (u32)G::R1 + row;
   u64* rowlds = lds + sub * H::ROWW;
   const LView<1, true> own{rowlds + grp * G::RS};
-  constexpr int SY = H::SYNC;
+  constexpr int SY = H::SYNC_ROUND, ST = H::SYNC_TENSOR;
 
   // forward row pass: round 0 from global, rounds exchange through LDS, last round stays in VGPRs
   u64 v[kE];
@@ -508,13 +695,13 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
     using Lay = Layout<G::N2, KB, LO>;
     const u32 tp = Lay::tpos(t);
     if constexpr (k == 0) {
-      const GView<1> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc};
+      const GView<1> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
       gin.template load<Lay>(v, tp);
     } else {
       lds_sync<SY>();
       own.template load<Lay>(v, tp);
     }
-    round_compute<G::N2, KB, LO, true, F>(v, tp, tf, base, q, {0, 0}, {0, 0});
+    round_compute<G::N2, KB, LO, true, F, true>(v, tp, tf, base, q, {0, 0}, {0, 0});
     if constexpr (k < Rd::NR - 1) {
       if (k > 0) lds_sync<SY>();
       own.template store<Lay>(v, tp);
@@ -525,17 +712,27 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   const u32 tpT = LayT::tpos(t);
   lds_sync<SY>();
   own.template store<LayT>(v, tpT);
-  lds_sync<SY>();
+  lds_sync<ST>();
+  // Montgomery products (t R^-1, in [0, 2q): the inverse rows take inputs below 3q); R is folded
+  // back in with N^-1 by the column inverse.  d1's sum of two products stays below 2q^2 < q R.
+  // Poly-major groups are whole wavefronts, so the group switch is a uniform branch per wave.
+  if constexpr (H::POLY_MAJOR) grp = __builtin_amdgcn_readfirstlane(grp);
   const bool active = grp < 3;
-  if (active) {
+  const u32 aoff = grp == 2 ? G::RS : 0, boff = grp == 2 ? 3 * G::RS : 2 * G::RS;
+  if (grp == 1) {
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
       const u32 idx = own.idx(tpT | LayT::jpos(j));
-      const u64 a0 = rowlds[idx], a1 = rowlds[G::RS + idx];
-      const u64 b0 = rowlds[2 * G::RS + idx], b1 = rowlds[3 * G::RS + idx];
-      if (grp == 0) v[j] = mulmod_barrett(a0, b0, m);
-      else if (grp == 1) v[j] = barrett_reduce((u128)a0 * b1 + (u128)a1 * b0, m);
-      else v[j] = mulmod_barrett(a1, b1, m);
+      const u128 t = (u128)rowlds[idx] * rowlds[3 * G::RS + idx] +
+                     (u128)rowlds[G::RS + idx] * rowlds[2 * G::RS + idx];
+      v[j] = mont_reduce_lazy((u64)t, (u64)(t >> 64), q, m.qinv);
+    }
+  } else if (active) {
+#pragma unroll
+    for (int j = 0; j < kE; ++j) {
+      const u32 idx = own.idx(tpT | LayT::jpos(j));
+      const u128 t = (u128)rowlds[aoff + idx] * rowlds[boff + idx];
+      v[j] = mont_reduce_lazy((u64)t, (u64)(t >> 64), q, m.qinv);
     }
   }
   // inverse row pass: its first round butterflies the low bits, the layout the tensor used
@@ -551,15 +748,41 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
       lds_sync<SY>();
       if (active) own.template load<Lay>(v, tp);
     }
-    if (active) round_compute<G::N2, KB, LO, false, kNotFinal>(v, tp, ti, base, q, {0, 0}, {0, 0});
+    if (active) round_compute<G::N2, KB, LO, false, kNotFinal, true>(v, tp, ti, base, q, {0, 0}, {0, 0});
     if constexpr (k == Rd::NR - 1) {
-      const GView<1> gout{d + ((u64)b * 3 + grp) * limbN + loc};
+      const GView<1> gout{d + ((u64)b * 3 + grp) * limbN + loc, 0};
       if (active) gout.template store<Lay>(v, tp);
     } else {
-      lds_sync<SY>();
+      // the first store into this slot must wait until every group has read it for the tensor
+      lds_sync<(k == 0 ? ST : SY)>();
       if (active) own.template store<Lay>(v, tp);
     }
   });
+}
+
+// One-generation grid for an item-loop kernel: as many workgroups as fit on the device at once
+// (occupancy queried once per kernel), never more than the items, rounded up to a multiple of 8
+// so item -> XCD placement holds (surplus workgroups exit at once).
+#ifndef FHE_ITEM_WG_PER_CU
+#define FHE_ITEM_WG_PER_CU 0  // 0: ask the occupancy API; > 0: A/B override
+#endif
+#ifndef FHE_ITEM_GENERATIONS
+#define FHE_ITEM_GENERATIONS 1
+#endif
+template <auto K, bool LOOP>
+dim3 item_grid(const fhe_ctx* c, int threads, u64 items) {
+  if (!LOOP) return dim3((u32)((items + 7) / 8 * 8));  // one workgroup per item
+  static const int per_cu = [threads] {
+    int nb = FHE_ITEM_WG_PER_CU;
+    if (nb == 0 &&
+        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, K, threads, 0) != hipSuccess || nb < 1))
+      nb = 1;
+    if (getenv("FHE_DEBUG_GRID")) fprintf(stderr, "item_grid: %d workgroups per CU\n", nb);
+    return nb * FHE_ITEM_GENERATIONS;
+  }();
+  u64 g = std::min<u64>(items, (u64)per_cu * (c->num_cus > 0 ? c->num_cus : 256));
+  g = (g + 7) / 8 * 8;
+  return dim3((u32)g);
 }
 
 template <int LOGN>
@@ -568,20 +791,20 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64* dst, u32 polys
   using G = Geo<LOGN>;
   const u64 pl = (u64)polys * nlimbs;
   const PolyMap pm = flat_map(pstride);
-  const dim3 gc((u32)(pl * G::TILES_C)), gr((u32)(pl * G::TILES_R));
+  const u64 ic = pl * G::TILES_C, ir = pl * G::TILES_R;
   if (fwd) {
-    k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(src, dst, nlimbs, limb0, pm, c->d_tw_fwd,
-                                                 c->d_nfold, c->d_mods);
+    k_ntt_col<LOGN, true><<<item_grid<k_ntt_col<LOGN, true>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
+        src, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd, c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_fwd");
-    k_ntt_row<LOGN, true><<<gr, G::THR_R, 0, s>>>(dst, dst, nlimbs, limb0, pm, c->d_tw_fwd,
-                                                 c->d_mods);
+    k_ntt_row<LOGN, true><<<item_grid<k_ntt_row<LOGN, true>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
+        dst, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_fwd, c->d_mods);
     prof_mark(s, "ntt_row_fwd");
   } else {
-    k_ntt_row<LOGN, false><<<gr, G::THR_R, 0, s>>>(src, dst, nlimbs, limb0, pm, c->d_tw_inv,
-                                                  c->d_mods);
+    k_ntt_row<LOGN, false><<<item_grid<k_ntt_row<LOGN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
+        src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv, c->d_mods);
     prof_mark(s, "ntt_row_inv");
-    k_ntt_col<LOGN, false><<<gc, G::THR_C, 0, s>>>(dst, dst, nlimbs, limb0, pm, c->d_tw_inv,
-                                                  c->d_nfold, c->d_mods);
+    k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
+        dst, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_inv, c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_inv");
   }
   FHE_HIP_CHECK(hipGetLastError());
@@ -597,20 +820,22 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   const u64 limbN = (u64)nlimbs * N;
   // x: [batch][4][nlimbs][N] workspace; A0, A1 -> slots 0, 1; B0, B1 -> slots 2, 3.
   const PolyMap to_x{2, 2 * limbN, limbN, 4 * limbN, limbN};
-  const dim3 gc((u32)((u64)batch * 2 * nlimbs * G::TILES_C));
-  k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(a, x, nlimbs, limb0, to_x, c->d_tw_fwd,
+  const u64 ic = (u64)batch * 2 * nlimbs * G::TILES_C;
+  const dim3 gc = item_grid<k_ntt_col<LOGN, true>, kLoopCol>(c, G::THR_C, ic);
+  k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(a, x, nlimbs, limb0, to_x, (u32)ic, c->d_tw_fwd,
                                                c->d_nfold, c->d_mods);
   prof_mark(s, "hm_col_fwd_a");
-  k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(b, x + 2 * limbN, nlimbs, limb0, to_x,
+  k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(b, x + 2 * limbN, nlimbs, limb0, to_x, (u32)ic,
                                                c->d_tw_fwd, c->d_nfold, c->d_mods);
   prof_mark(s, "hm_col_fwd_b");
   const dim3 gh((u32)((u64)batch * nlimbs * H::TILES));
   k_hommult_row<LOGN><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd, c->d_tw_inv,
                                             c->d_mods);
   prof_mark(s, "hm_row_tensor");
-  const dim3 gi((u32)((u64)batch * 3 * nlimbs * G::TILES_C));
-  k_ntt_col<LOGN, false><<<gi, G::THR_C, 0, s>>>(d, d, nlimbs, limb0, flat_map(limbN),
-                                                c->d_tw_inv, c->d_nfold, c->d_mods);
+  const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
+  // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
+  k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, kLoopCol>(c, G::THR_C, ii), G::THR_C, 0, s>>>(
+      d, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv, c->d_nfold + 2, c->d_mods);
   prof_mark(s, "hm_col_inv");
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;

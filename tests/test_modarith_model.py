@@ -1,0 +1,93 @@
+"""CPU models of the word-level reductions in gpu-fhe_amd/csrc/modarith.hpp, checked against
+exact big-integer arithmetic: the range claims the lazy NTT butterflies rely on (FHE_BFLY = 2 in
+csrc/ntt.hip) and the Montgomery tensor of the fused HomMult kernel.  Each model follows the
+device code's 32-bit partial products step by step (same truncations, same carries)."""
+import random
+
+import pytest
+
+import sys, os
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+import pyoracle  # noqa: E402
+
+M32, M64 = (1 << 32) - 1, (1 << 64) - 1
+
+
+def shoup_q3(y, w, ws, q):
+    """modarith.hpp shoup_q3: quotient from three partial products, remainder mod 2^64."""
+    y0, y1 = y & M32, y >> 32
+    s0, s1 = ws & M32, ws >> 32
+    a = y1 * s0                      # v_mad_u64_u32 (y1, s0, 0)
+    bfull = y0 * s1 + a              # v_mad_u64_u32 with carry-out
+    b, c = bfull & M64, bfull >> 64
+    h = (y1 * s1 + ((c << 32) | (b >> 32))) & M64
+    nq = (-q) & M64
+    w0, w1, n0, n1 = w & M32, w >> 32, nq & M32, nq >> 32
+    h0, h1 = h & M32, h >> 32
+    t = (h0 * n0 + y0 * w0) & M64
+    hi = ((t >> 32) + y1 * w0 + y0 * w1 + h1 * n0 + h0 * n1) & M32
+    return (hi << 32) | (t & M32)
+
+
+def mont_reduce_lazy(t, q):
+    """modarith.hpp mont_reduce_lazy with R = 2^64: t R^-1 mod q up to one q."""
+    qinv = (-pow(q, -1, 1 << 64)) & M64
+    tlo, thi = t & M64, t >> 64
+    m = (tlo * qinv) & M64
+    return (thi + ((m * q) >> 64) + (1 if tlo else 0)) & M64
+
+
+def _moduli():
+    qs = pyoracle.gen_moduli(16, 4) + pyoracle.gen_moduli(10, 2)
+    qs.append(pyoracle.gen_moduli(10, 1, bits=61)[0])  # the largest size ctx_create accepts
+    return qs
+
+
+@pytest.mark.parametrize("q", _moduli())
+def test_shoup_q3_range_and_congruence(q):
+    rng = random.Random(q)
+    ws_of = lambda w: (w << 64) // q  # noqa: E731
+    edge_y = [0, 1, q - 1, 3 * q - 1, 8 * q - 1, M64, M64 - 1, 1 << 63]
+    edge_w = [0, 1, q - 1, q // 2]
+    cases = [(y, w) for y in edge_y for w in edge_w]
+    cases += [(rng.getrandbits(64), rng.randrange(q)) for _ in range(3000)]
+    for y, w in cases:
+        r = shoup_q3(y, w, ws_of(w), q)
+        assert 0 <= r < 3 * q, (y, w)
+        assert r % q == (y * w) % q, (y, w)
+
+
+@pytest.mark.parametrize("q", _moduli())
+def test_mont_reduce_lazy(q):
+    rng = random.Random(q + 1)
+    R_inv = pow(1 << 64, -1, q)
+    cases = [0, 1, q * q - 1, 2 * q * q - 1, q << 64 - 1]
+    cases += [rng.randrange(q) * rng.randrange(q) for _ in range(2000)]
+    cases += [rng.randrange(q) * rng.randrange(q) + rng.randrange(q) * rng.randrange(q)
+              for _ in range(2000)]  # d1 = a0 b1 + a1 b0 < 2 q^2
+    for t in cases:
+        r = mont_reduce_lazy(t, q)
+        assert 0 <= r < 2 * q, t
+        assert r % q == (t * R_inv) % q, t
+
+
+@pytest.mark.parametrize("q", _moduli())
+def test_lazy_butterfly_ranges(q):
+    """Forward CT values stay in [0, 8q) and inverse GS values in [0, 3q) (FHE_BFLY = 2)."""
+    rng = random.Random(q + 2)
+    for _ in range(2000):
+        w = rng.randrange(q)
+        ws = (w << 64) // q
+        x, y = rng.randrange(8 * q), rng.randrange(8 * q)
+        u = x - 4 * q if x >= 4 * q else x
+        v = shoup_q3(y, w, ws, q)
+        a, b = u + v, u - v + 3 * q
+        assert 0 <= a < 8 * q and 0 < b < 8 * q and a < 1 << 64
+        assert (a - (x + w * y)) % q == 0 and (b - (x - w * y)) % q == 0
+        x, y = rng.randrange(3 * q), rng.randrange(3 * q)
+        s = x + y
+        s = s - 3 * q if s >= 3 * q else s
+        d = shoup_q3(x - y + 3 * q, w, ws, q)
+        assert 0 <= s < 3 * q and 0 <= d < 3 * q
+        assert (d - (x - y) * w) % q == 0
