@@ -237,4 +237,47 @@ int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t
   return launch_keyswitch_shard(c, ks0, ks1, c_all, d2, evk_b, evk_a, 0, c->L, batch, ws, hs(s));
 }
 
+size_t fhe_rescale_workspace(const fhe_ctx* c, uint32_t polys, uint32_t nlimbs) {
+  return c ? rescale_workspace_bytes(c, polys, nlimbs) : 0;
+}
+
+int fhe_rescale(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t polys,
+                uint32_t nlimbs, int ntt_form, void* ws, fhe_stream_t s) {
+  int rc = check_window(c, 0, nlimbs, c ? c->L : 0, "fhe_rescale");
+  if (rc) return rc;
+  if (ntt_form && (rc = ensure_ws(c, rescale_workspace_bytes(c, polys, nlimbs), &ws))) return rc;
+  return launch_rescale(c, out, in, polys, nlimbs, ntt_form != 0, ws, hs(s));
+}
+
+int fhe_automorphism(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t polys,
+                     uint32_t limb0, uint32_t nlimbs, uint32_t galois_elt, int ntt_form,
+                     fhe_stream_t s) {
+  int rc = check_window(c, limb0, nlimbs, c ? c->L + c->K : 0, "fhe_automorphism");
+  if (rc) return rc;
+  if (out == in && polys && nlimbs) {
+    set_error("fhe_automorphism: out must not alias in");
+    return kInvalid;
+  }
+  const uint64_t stride = (uint64_t)nlimbs * c->n;
+  return launch_automorphism(c, out, stride, in, stride, polys, limb0, nlimbs, galois_elt,
+                             ntt_form != 0, hs(s));
+}
+
+size_t fhe_rotate_workspace(const fhe_ctx* c, uint32_t batch) {
+  return c ? rotate_workspace_bytes(c, batch) : 0;
+}
+
+int fhe_rotate(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t galois_elt,
+               const uint64_t* rot_b, const uint64_t* rot_a, uint32_t batch, void* ws,
+               fhe_stream_t s) {
+  int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_rotate");
+  if (rc) return rc;
+  if (out == in && batch) {
+    set_error("fhe_rotate: out must not alias in");
+    return kInvalid;
+  }
+  if ((rc = ensure_ws(c, rotate_workspace_bytes(c, batch), &ws))) return rc;
+  return launch_rotate(c, out, in, galois_elt, rot_b, rot_a, batch, ws, hs(s));
+}
+
 }  // extern "C"

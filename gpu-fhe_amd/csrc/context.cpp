@@ -135,6 +135,9 @@ ModParams make_mod_params(u64 q) {
     for (int i = 0; i < 5; ++i) inv *= 2 - q * inv;
     m.qinv = 0 - inv;
   }
+  m.r64 = (u64)(((u128)1 << 64) % q);
+  m.r64s = (u64)(((u128)m.r64 << 64) / q);
+  m.ones = (u64)(((u128)1 << 64) / q);
   return m;
 }
 
@@ -244,7 +247,8 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
   if ((rc = upload(&c->d_mods, c->mods_host.data(), M)) ||
       (rc = upload(&c->d_tw_fwd, twf.data(), M * n)) ||
       (rc = upload(&c->d_tw_inv, twi.data(), M * n)) ||
-      (rc = upload(&c->d_nfold, nfold.data(), 4 * M)) || (rc = build_rns_tables(c))) {
+      (rc = upload(&c->d_nfold, nfold.data(), 4 * M)) || (rc = build_rns_tables(c)) ||
+      (rc = build_galois_tables(c))) {
     ctx_destroy(c);
     return rc;
   }
@@ -257,7 +261,8 @@ int ctx_destroy(fhe_ctx* c) {
   (void)hipSetDevice(c->device);
   for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_inv, (void*)c->d_nfold,
                     (void*)c->d_modup_inv, (void*)c->d_modup_hat, (void*)c->d_moddown_inv,
-                    (void*)c->d_moddown_hat, (void*)c->d_pinv, c->workspace})
+                    (void*)c->d_moddown_hat, (void*)c->d_pinv, (void*)c->d_rs_tab,
+                    (void*)c->d_rs_half, c->workspace})
     if (ptr) (void)hipFree(ptr);
   delete c;
   return kOk;

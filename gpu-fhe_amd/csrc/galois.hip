@@ -1,0 +1,251 @@
+// Rescale (divide-and-round by the last modulus) and Galois automorphisms / rotation for gfx950:
+// SURVEY.md §8(f) row 1, the first ciphertext operations after the north-star path.
+//
+// Not in the reference (its only ciphertext operation is poly_add, /root/reference/ polynomial.py:3-5);
+// the definitions are the standard RNS-CKKS ones, restated in oracle/pyoracle.py
+// (rescale_coeff / rescale_ntt, automorphism_coeff / automorphism_ntt, rotate):
+//   rescale   out_i = (x_i - ((x_last + h) mod q_last - h)) q_last^-1 mod q_i,  h = q_last / 2
+//             = floor((X + h) / q_last) mod q_i for the CRT value X (divide and round);
+//   sigma_k   a(X) -> a(X^k), k odd: coefficient i -> i k mod 2N (negated past N); in the NTT
+//             domain a gather, slot j <- slot brv(((2 brv(j) + 1) k mod 2N - 1) / 2);
+//   rotate    (sigma_k c0 + KS0(sigma_k c1), KS1(sigma_k c1)) with the key for sigma_k(s) -> s.
+// All HBM-bound elementwise / gather passes (the rotation's cost is its key-switch).
+#include "internal.hpp"
+
+namespace fhe {
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ u32 brv(u32 x, u32 bits) { return __builtin_bitreverse32(x) >> (32 - bits); }
+
+// t < 2^64 -> t mod q, any q < 2^61 (Shoup by 1: [0, 3q), then two subtractions)
+__device__ __forceinline__ u64 reduce_word(u64 t, const ModParams& m) {
+  u64 r = shoup_q3(t, 1, m.ones, 0 - m.q);
+  r = csub(r, 2 * m.q);
+  return csub(r, m.q);
+}
+
+// Grid: x over coefficients, y = limb, z = poly.  in/out rows at stride N, polys at pin / pout.
+__global__ __launch_bounds__(kThreads) void k_automorph(u64* __restrict__ out, u64 pout,
+                                                        const u64* __restrict__ in, u64 pin,
+                                                        u32 nlimbs, u32 limb0, u32 log_n, u32 k,
+                                                        int ntt, const ModParams* __restrict__ mods) {
+  const u64 n = 1ull << log_n;
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 l = blockIdx.y;
+  const u64 p = blockIdx.z;
+  const u64* row = in + p * pin + (u64)l * n;
+  u64 v;
+  if (ntt) {
+    const u32 mask2 = (2u << log_n) - 1;
+    const u32 e = ((2 * brv(c, log_n) + 1) * k) & mask2;  // k odd, e odd
+    v = row[brv((e - 1) >> 1, log_n)];
+  } else {
+    const u32 mask2 = (2u << log_n) - 1;
+    const u32 i = (c * k) & mask2;  // here k = kinv: the source of output coefficient c
+    const u64 q = mods[limb0 + l].q;
+    if (i < n) {
+      v = row[i];
+    } else {
+      const u64 x = row[i - n];
+      v = x ? q - x : 0;
+    }
+  }
+  out[p * pout + (u64)l * n + c] = v;
+}
+
+// Rescale, coefficient form: in [polys][nl][N] -> out [polys][nl - 1][N].  Grid: x over
+// coefficients, y = out limb i, z = poly.  tab[i] = {Shoup pair of q_last^-1 mod q_i}, half[i] =
+// h mod q_i.
+__global__ __launch_bounds__(kThreads) void k_rescale_coeff(u64* __restrict__ out,
+                                                            const u64* __restrict__ in, u32 nl,
+                                                            u32 log_n,
+                                                            const ulonglong2* __restrict__ tab,
+                                                            const u64* __restrict__ half,
+                                                            const ModParams* __restrict__ mods) {
+  const u64 n = 1ull << log_n;
+  const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 i = blockIdx.y;
+  const u64 p = blockIdx.z;
+  const ModParams ml = mods[nl - 1], mi = mods[i];
+  const u64 h = ml.q >> 1;
+  const u64 t = csub(in[(p * nl + nl - 1) * n + c] + h, ml.q);
+  const u64 tmp = csub(reduce_word(t, mi) + mi.q - half[i], mi.q);
+  const u64 d = in[(p * nl + i) * n + c] + mi.q - tmp;
+  const ulonglong2 w = tab[i];
+  out[(p * (nl - 1) + i) * n + c] = csub(shoup_lazy(d, w.x, w.y, mi.q), mi.q);
+}
+
+// Rescale, NTT form, step 1: last [polys][N] (coefficient form of the last limb) ->
+// tmp [polys][nl - 1][N] = ((last + h) mod q_last - h) mod q_i (to be NTT'd over limbs 0..nl-2).
+__global__ __launch_bounds__(kThreads) void k_rescale_spread(u64* __restrict__ tmp,
+                                                             const u64* __restrict__ last, u32 nl,
+                                                             u32 log_n,
+                                                             const u64* __restrict__ half,
+                                                             const ModParams* __restrict__ mods) {
+  const u64 n = 1ull << log_n;
+  const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 i = blockIdx.y;
+  const u64 p = blockIdx.z;
+  const ModParams ml = mods[nl - 1], mi = mods[i];
+  const u64 t = csub(last[p * n + c] + (ml.q >> 1), ml.q);
+  tmp[(p * (nl - 1) + i) * n + c] = csub(reduce_word(t, mi) + mi.q - half[i], mi.q);
+}
+
+// Rescale, NTT form, step 2: out_i = (x_i - tmp_i) q_last^-1 mod q_i.
+__global__ __launch_bounds__(kThreads) void k_rescale_finish(u64* __restrict__ out,
+                                                             const u64* __restrict__ in,
+                                                             const u64* __restrict__ tmp, u32 nl,
+                                                             u32 log_n,
+                                                             const ulonglong2* __restrict__ tab,
+                                                             const ModParams* __restrict__ mods) {
+  const u64 n = 1ull << log_n;
+  const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 i = blockIdx.y;
+  const u64 p = blockIdx.z;
+  const u64 q = mods[i].q;
+  const u64 d = in[(p * nl + i) * n + c] + q - tmp[(p * (nl - 1) + i) * n + c];
+  const ulonglong2 w = tab[i];
+  out[(p * (nl - 1) + i) * n + c] = csub(shoup_lazy(d, w.x, w.y, q), q);
+}
+
+// Rotation combine: out[b][0] = (out[b][0] + ks0[b]) mod q, out[b][1] = ks1[b] (out[b][0] already
+// holds sigma_k(c0)).  Grid: x over coefficients, y = limb, z = ciphertext.
+__global__ __launch_bounds__(kThreads) void k_rotate_combine(u64* __restrict__ out,
+                                                             const u64* __restrict__ ks0,
+                                                             const u64* __restrict__ ks1, u32 L,
+                                                             u32 log_n,
+                                                             const ModParams* __restrict__ mods) {
+  const u64 n = 1ull << log_n;
+  const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 l = blockIdx.y;
+  const u64 b = blockIdx.z;
+  const u64 q = mods[l].q;
+  const u64 ln = (u64)L * n, e = b * ln + (u64)l * n + c;
+  u64* o = out + b * 2 * ln + (u64)l * n + c;
+  o[0] = csub(o[0] + ks0[e], q);
+  o[ln] = ks1[e];
+}
+
+inline u64 modinv_u64(u64 a, u64 q) { return powmod_u64(a % q, q - 2, q); }
+
+// k^-1 mod 2^bits for odd k (Newton: each step doubles the correct low bits)
+inline u32 modinv_odd_pow2(u32 k, u32 bits) {
+  u32 inv = k;
+  for (int i = 0; i < 5; ++i) inv *= 2 - k * inv;
+  return inv & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1));
+}
+
+}  // namespace
+
+int build_galois_tables(fhe_ctx* c) {
+  // rescale tables for every last limb l in [1, L): entry [l][i], i < l
+  const u32 L = c->L;
+  std::vector<ulonglong2> tab((size_t)L * L, ulonglong2{0, 0});
+  std::vector<u64> half((size_t)L * L, 0);
+  for (u32 l = 1; l < L; ++l) {
+    const u64 ql = c->moduli[l];
+    for (u32 i = 0; i < l; ++i) {
+      const u64 q = c->moduli[i];
+      const u64 inv = modinv_u64(ql, q);
+      tab[(size_t)l * L + i] = ulonglong2{inv, (u64)(((u128)inv << 64) / q)};
+      half[(size_t)l * L + i] = (ql >> 1) % q;
+    }
+  }
+  FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c->d_rs_tab), tab.size() * sizeof(ulonglong2)));
+  FHE_HIP_CHECK(hipMemcpy(c->d_rs_tab, tab.data(), tab.size() * sizeof(ulonglong2),
+                          hipMemcpyHostToDevice));
+  FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c->d_rs_half), half.size() * sizeof(u64)));
+  FHE_HIP_CHECK(hipMemcpy(c->d_rs_half, half.data(), half.size() * sizeof(u64), hipMemcpyHostToDevice));
+  return kOk;
+}
+
+int launch_automorphism(const fhe_ctx* c, u64* out, u64 pout, const u64* in, u64 pin, u32 polys,
+                        u32 limb0, u32 nlimbs, u32 galois_elt, bool ntt, hipStream_t s) {
+  const u32 two_n = 2u << c->log_n;
+  if ((galois_elt & 1) == 0 || galois_elt >= two_n) {
+    set_error("automorphism: the Galois element must be odd and below 2N");
+    return kInvalid;
+  }
+  if ((u64)polys * nlimbs == 0) return kOk;
+  // coefficient form gathers through k^-1 mod 2N (odd elements form a group mod 2^(logN+1))
+  u32 k = galois_elt;
+  if (!ntt) k = (u32)modinv_odd_pow2(galois_elt, c->log_n + 1);
+  const dim3 g((u32)(c->n / kThreads), nlimbs, polys);
+  k_automorph<<<g, kThreads, 0, s>>>(out, pout, in, pin, nlimbs, limb0, c->log_n, k, ntt ? 1 : 0,
+                                     c->d_mods);
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+
+size_t rescale_workspace_bytes(const fhe_ctx* c, u32 polys, u32 nl) {
+  return (size_t)polys * nl * c->n * sizeof(u64);
+}
+
+int launch_rescale(const fhe_ctx* c, u64* out, const u64* in, u32 polys, u32 nl, bool ntt,
+                   void* ws, hipStream_t s) {
+  if (nl < 2 || nl > c->L) {
+    set_error("rescale: need 2 <= limbs <= L (the input spans Q-limbs 0 .. limbs-1)");
+    return kInvalid;
+  }
+  if (polys == 0) return kOk;
+  const u64 n = c->n;
+  const ulonglong2* tab = c->d_rs_tab + (size_t)(nl - 1) * c->L;
+  const u64* half = c->d_rs_half + (size_t)(nl - 1) * c->L;
+  const dim3 g((u32)(n / kThreads), nl - 1, polys);
+  if (!ntt) {
+    k_rescale_coeff<<<g, kThreads, 0, s>>>(out, in, nl, c->log_n, tab, half, c->d_mods);
+    FHE_HIP_CHECK(hipGetLastError());
+    return kOk;
+  }
+  // NTT form: INTT of the last limb, spread it over the other limbs, NTT those, finish
+  u64* last = static_cast<u64*>(ws);           // [polys][N]
+  u64* tmp = last + (u64)polys * n;            // [polys][nl - 1][N]
+  int rc;
+  if ((rc = launch_ntt_strided(c, false, in + (u64)(nl - 1) * n, (u64)nl * n, last, n, polys,
+                                nl - 1, 1, s)))
+    return rc;
+  k_rescale_spread<<<g, kThreads, 0, s>>>(tmp, last, nl, c->log_n, half, c->d_mods);
+  FHE_HIP_CHECK(hipGetLastError());
+  if ((rc = launch_ntt(c, true, tmp, tmp, polys, (u64)(nl - 1) * n, 0, nl - 1, s))) return rc;
+  k_rescale_finish<<<g, kThreads, 0, s>>>(out, in, tmp, nl, c->log_n, tab, c->d_mods);
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+
+size_t rotate_workspace_bytes(const fhe_ctx* c, u32 batch) {
+  // sigma(c1) [batch][L][N], ks0 and ks1 [batch][L][N], then the key-switch's own workspace
+  return 3 * (size_t)batch * c->L * c->n * sizeof(u64) + keyswitch_workspace_bytes(c, c->L, batch);
+}
+
+int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, const u64* rot_b,
+                  const u64* rot_a, u32 batch, void* ws, hipStream_t s) {
+  if (c->K == 0) {
+    set_error("rotate: context has no special primes (K = 0)");
+    return kInvalid;
+  }
+  if (batch == 0) return kOk;
+  const u32 L = c->L;
+  const u64 n = c->n, ln = (u64)L * n;
+  u64* sc1 = static_cast<u64*>(ws);  // [batch][L][N]
+  u64* ks0 = sc1 + batch * ln;
+  u64* ks1 = ks0 + batch * ln;
+  u64* kws = ks1 + batch * ln;
+  int rc;
+  if ((rc = launch_automorphism(c, out, 2 * ln, in, 2 * ln, batch, 0, L, galois_elt, true, s)) ||
+      (rc = launch_automorphism(c, sc1, ln, in + ln, 2 * ln, batch, 0, L, galois_elt, true, s)))
+    return rc;
+  // key-switch sigma(c1): its coefficient form goes to the tail of the key-switch workspace
+  const size_t kbytes = keyswitch_workspace_bytes(c, L, batch);
+  u64* c_all = reinterpret_cast<u64*>(reinterpret_cast<char*>(kws) + kbytes) - batch * ln;
+  if ((rc = launch_ntt_strided(c, false, sc1, ln, c_all, ln, batch, 0, L, s))) return rc;
+  if ((rc = launch_keyswitch_shard(c, ks0, ks1, c_all, sc1, rot_b, rot_a, 0, L, batch, kws, s)))
+    return rc;
+  k_rotate_combine<<<dim3((u32)(n / kThreads), L, batch), kThreads, 0, s>>>(out, ks0, ks1, L,
+                                                                           c->log_n, c->d_mods);
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+
+}  // namespace fhe

@@ -43,6 +43,9 @@ struct fhe_ctx {
   // [L + K][4] Shoup pairs: N^-1, psi^-1 N^-1 (last inverse stage), and the same times
   // R = 2^64 (HomMult's inverse, undoing the Montgomery tensor's R^-1)
   ulonglong2* d_nfold = nullptr;
+  // rescale: [L][L] Shoup pairs of q_l^-1 mod q_i and (q_l / 2) mod q_i, row l = last limb
+  ulonglong2* d_rs_tab = nullptr;
+  uint64_t* d_rs_half = nullptr;
 
   // Hybrid key-switch base-conversion constants (rns.hip), Shoup pairs, device resident.
   // Digit j covers Q-limbs [j * alpha, min(L, (j + 1) * alpha)).
@@ -62,6 +65,9 @@ namespace fhe {
 // data layout [polys][nlimbs][N] with poly stride `pstride` (elements); limb l uses table limb0 + l.
 int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 polys, u64 pstride,
                u32 limb0, u32 nlimbs, hipStream_t s);
+// the same with separate source / destination poly strides
+int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
+                       u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
 // Fused ct x ct tensor: a, b [batch][2][nlimbs][N] coefficient form -> d [batch][3][nlimbs][N].
 int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                    u32 nlimbs, void* ws, hipStream_t s);
@@ -87,6 +93,20 @@ size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch);
 // out [T][N] over limbs [t0, t0+T) (ranges disjoint).
 int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u32 t0, u32 T,
                     hipStream_t s);
+
+// ---- launchers (galois.hip): SURVEY.md §8(f) row 1 -------------------------------------
+int build_galois_tables(fhe_ctx* c);
+// sigma_k on [polys][nlimbs][N] rows (poly strides pin / pout), NTT or coefficient form
+int launch_automorphism(const fhe_ctx* c, u64* out, u64 pout, const u64* in, u64 pin, u32 polys,
+                        u32 limb0, u32 nlimbs, u32 galois_elt, bool ntt, hipStream_t s);
+// divide-and-round by q_{nl-1}: in [polys][nl][N] (Q-limbs 0..nl-1) -> out [polys][nl-1][N]
+int launch_rescale(const fhe_ctx* c, u64* out, const u64* in, u32 polys, u32 nl, bool ntt,
+                   void* ws, hipStream_t s);
+size_t rescale_workspace_bytes(const fhe_ctx* c, u32 polys, u32 nl);
+// in/out [batch][2][L][N] NTT form; rot_b/rot_a [dnum][L + K][N] (key for sigma_k(s) -> s)
+int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, const u64* rot_b,
+                  const u64* rot_a, u32 batch, void* ws, hipStream_t s);
+size_t rotate_workspace_bytes(const fhe_ctx* c, u32 batch);
 
 // ---- host (context.cpp) ----------------------------------------------------------------
 int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 K, u32 dnum,

@@ -29,6 +29,9 @@ struct ModParams {
   u32 sh_a;  // bitlen - 1
   u32 sh_b;  // bitlen + 3  (= b - a)
   u64 qinv;  // Montgomery (R = 2^64): -q^-1 mod 2^64 for odd q, else 0
+  u64 r64;   // 2^64 mod q, and its Shoup companion floor(r64 2^64 / q)
+  u64 r64s;
+  u64 ones;  // floor(2^64 / q): the Shoup companion of 1 (a 64-bit word mod q)
 };
 
 __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return (u64)(((u128)a * b) >> 64); }
@@ -142,6 +145,18 @@ __device__ __forceinline__ u64 mulmod_barrett(u64 a, u64 b, const ModParams& m) 
 __device__ __forceinline__ u64 mont_reduce_lazy(u64 tlo, u64 thi, u64 q, u64 qinv) {
   const u64 m = tlo * qinv;
   return thi + mulhi64(m, q) + (tlo != 0 ? 1 : 0);
+}
+
+// Full reduction of a 128-bit z = (zhi, zlo) with zhi < 2^64 (any value) into [0, q), q < 2^61:
+// zhi 2^64 + zlo = zhi (2^64 mod q) + zlo, both terms by the 3-product Shoup (into [0, 3q) each),
+// then three conditional subtractions.  The key-switch inner product accumulates up to 16
+// products of residues (< 16 q^2 < 2^126) and reduces once.
+__device__ __forceinline__ u64 reduce128(u64 zlo, u64 zhi, const ModParams& m) {
+  const u64 nq = 0 - m.q;
+  u64 r = shoup_q3(zhi, m.r64, m.r64s, nq) + shoup_q3(zlo, 1, m.ones, nq);
+  r = csub(r, 4 * m.q);
+  r = csub(r, 2 * m.q);
+  return csub(r, m.q);
 }
 
 // Full reduction of any 64-bit x into [0, q), any q >= 2: Barrett for 2^31 <= q < 2^61

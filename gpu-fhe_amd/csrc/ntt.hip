@@ -39,6 +39,12 @@ namespace {
 constexpr int kElog = FHE_ELOG;
 constexpr int kE = 1 << kElog;
 constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per workgroup
+// FHE_COL_THREADS: column-pass workgroup size; more threads = wider tiles (16 columns per 256
+// threads at N = 2^16), i.e. longer contiguous runs per row in HBM, at the same LDS per wave.
+#ifndef FHE_COL_THREADS
+#define FHE_COL_THREADS kThreads
+#endif
+constexpr int kColThreads = FHE_COL_THREADS;
 // FHE_NTT_ABLATE (timing-only A/B builds, tools/build_variant.sh; never the shipped library):
 // 1 = skip the butterflies of the generic passes, 2 = skip their global loads/stores,
 // 3 = row passes read row 0's twiddles for every row (wrong results; twiddle-fetch cost).
@@ -139,7 +145,9 @@ struct Layout {
   }
 };
 
-enum Final : int { kNotFinal = 0, kFinalFwd = 1, kFinalInv = 2 };
+// kFinalFwd reduces the last forward stage to [0, q); kFinalFwd2 only to [0, 2q) (the fused
+// HomMult tensor: its Montgomery products accept operands below 2q).
+enum Final : int { kNotFinal = 0, kFinalFwd = 1, kFinalInv = 2, kFinalFwd2 = 3 };
 
 // LDS exchange fences.  A row sub-transform's threads all sit in one wavefront, so the row
 // kernels only need wavefront-scope ordering of their LDS traffic (DS instructions of one wave
@@ -181,13 +189,20 @@ __device__ __forceinline__ void xcd_limb_split(u32 b, u32 nlimbs, u32& limb, u32
 
 // Maps a launch's poly index p to element offsets: p = g * pg + k reads src + g*sgs + k*sps and
 // writes dst + g*dgs + k*dps (lets HomMult scatter a/b into its 4-slot workspace).
+// With alt > 0, the polys k >= alt of each group read the second source at k - alt instead
+// (HomMult's column-forward reads a's two polys and b's two polys of a ciphertext in one launch).
 struct PolyMap {
   u32 pg;
   u64 sgs, sps, dgs, dps;
+  u32 alt = 0;
   __device__ __forceinline__ u64 src(u32 p) const { return (u64)(p / pg) * sgs + (u64)(p % pg) * sps; }
   __device__ __forceinline__ u64 dst(u32 p) const { return (u64)(p / pg) * dgs + (u64)(p % pg) * dps; }
+  __device__ __forceinline__ bool second(u32 p) const { return alt != 0 && p % pg >= alt; }
+  __device__ __forceinline__ u64 src2(u32 p) const {
+    return (u64)(p / pg) * sgs + (u64)(p % pg - alt) * sps;
+  }
 };
-static inline PolyMap flat_map(u64 pstride) { return PolyMap{1, pstride, 0, pstride, 0}; }
+static inline PolyMap flat_map(u64 pstride) { return PolyMap{1, pstride, 0, pstride, 0, 0}; }
 
 // The distinct twiddles of one round: butterfly (stage b, pair j) uses twiddle group
 // g = (tp | jpos(j)) >> (LO + b + 1); slot[b][j] numbers the distinct (b, g - tp part) pairs and
@@ -298,14 +313,15 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
 #endif
       }
     }
-    if constexpr (FIN == kFinalFwd) {
+    if constexpr (FIN == kFinalFwd || FIN == kFinalFwd2) {
 #pragma unroll
       for (int j = 0; j < E; ++j) {
 #if FHE_BFLY == 2
-        x[j] = csub(csub(csub(x[j], q4), q2), q);
+        x[j] = csub(csub(x[j], q4), q2);
 #else
-        x[j] = csub(csub(x[j], q2), q);
+        x[j] = csub(x[j], q2);
 #endif
+        if constexpr (FIN == kFinalFwd) x[j] = csub(x[j], q);
       }
     }
   } else {
@@ -477,8 +493,10 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
       gout.template store<Lay>(x, tp);
 #endif
     } else {
-      // round 0's store needs a fence only when the previous item's last LDS reads precede it
-      if (k > 0 || LOOPED) lds_sync<SYNC>();
+      // round 0's store needs a fence only when the previous item's last LDS reads precede it;
+      // the (free) wave-local fence also keeps the row passes' LDS stores together after the
+      // butterflies, which measured faster than letting them interleave
+      if (k > 0 || LOOPED || SYNC == kWaveSync) lds_sync<SYNC>();
       lv.template store<Lay>(x, tp);
     }
   });
@@ -490,7 +508,7 @@ struct Geo {
   static constexpr int R1 = 1 << N1, R2 = 1 << N2;  // R1 rows x R2 columns
   // column pass: SUBS_C columns per workgroup, lanes run over columns
   static constexpr int TPS_C = R1 >> kElog;
-  static constexpr int SUBS_C = (kThreads / TPS_C) < R2 ? (kThreads / TPS_C) : R2;
+  static constexpr int SUBS_C = (kColThreads / TPS_C) < R2 ? (kColThreads / TPS_C) : R2;
   static constexpr int THR_C = SUBS_C * TPS_C;
   static constexpr int CS = SUBS_C + 1;  // LDS row stride (words)
   static constexpr int LDS_C = R1 * CS;
@@ -513,7 +531,9 @@ struct Geo {
 
 // Column pass over items (p, l, tile) of src/dst [polys][nlimbs][N] via PolyMap.
 template <int LOGN, bool FWD>
-__global__ FHE_KATTR void k_ntt_col(const u64* __restrict__ src,
+__global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
+    FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_ntt_col(const u64* __restrict__ src,
+                                                      const u64* __restrict__ src2,
                                                       u64* __restrict__ dst, u32 nlimbs,
                                                       u32 limb0, PolyMap pm, u32 items,
                                                       const ulonglong2* __restrict__ tw_all,
@@ -526,25 +546,27 @@ __global__ FHE_KATTR void k_ntt_col(const u64* __restrict__ src,
   const LView<G::CS, false> lv{lds + sub};
   struct Item {  // all wave-uniform
     u32 limb;
-    u64 src, dst;
+    const u64* s;
+    u64* d;
   };
   auto decode = [&](u32 it) {
     const u32 tile = it % G::TILES_C, pl = it / G::TILES_C;
     const u32 l = pl % nlimbs, p = pl / nlimbs;
     const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
-    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), pm.src(p) + loc, pm.dst(p) + loc};
+    const u64* s = pm.second(p) ? src2 + pm.src2(p) : src + pm.src(p);
+    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), s + loc, dst + pm.dst(p) + loc};
   };
   u32 it = blockIdx.x;
   if (it >= items) return;
   Item cur = decode(it);
   u64 x[kE], y[kE];
-  pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(src) + cur.src, sub}, t, x);
+  pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(cur.s), sub}, t, x);
   while (true) {
     const u32 nx = it + gridDim.x;
     const bool more = kLoopCol && nx < items;
     const Item nxt = more ? decode(nx) : cur;
     auto prefetch = [&] {
-      if (more) pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(src) + nxt.src, sub}, t, y);
+      if (more) pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(nxt.s), sub}, t, y);
     };
     ulonglong2 nf0 = {0, 0}, nf1 = {0, 0};
     if (!FWD) {
@@ -552,7 +574,7 @@ __global__ FHE_KATTR void k_ntt_col(const u64* __restrict__ src,
       nf1 = nfold[4 * cur.limb + 1];
     }
     pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol>(
-        x, GView<G::R2>{dst + cur.dst, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
+        x, GView<G::R2>{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
         nf0, nf1, prefetch);
     if (!more) break;
     it = nx;
@@ -691,7 +713,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
     constexpr int k = decltype(kc)::value;
     constexpr int KB = Rd::kb(k);
     constexpr int LO = Rd::lo_fwd(k);
-    constexpr int F = (k == Rd::NR - 1) ? kFinalFwd : kNotFinal;
+    constexpr int F = (k == Rd::NR - 1) ? kFinalFwd2 : kNotFinal;
     using Lay = Layout<G::N2, KB, LO>;
     const u32 tp = Lay::tpos(t);
     if constexpr (k == 0) {
@@ -713,8 +735,9 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   lds_sync<SY>();
   own.template store<LayT>(v, tpT);
   lds_sync<ST>();
-  // Montgomery products (t R^-1, in [0, 2q): the inverse rows take inputs below 3q); R is folded
-  // back in with N^-1 by the column inverse.  d1's sum of two products stays below 2q^2 < q R.
+  // Montgomery products of the forward outputs (in [0, 2q)): t R^-1 in [0, 2q), which the inverse
+  // rows take (inputs below 3q); R is folded back in with N^-1 by the column inverse.  d1's sum of
+  // two products stays below 8q^2 < q R (q < 2^61).
   // Poly-major groups are whole wavefronts, so the group switch is a uniform branch per wave.
   if constexpr (H::POLY_MAJOR) grp = __builtin_amdgcn_readfirstlane(grp);
   const bool active = grp < 3;
@@ -786,25 +809,27 @@ dim3 item_grid(const fhe_ctx* c, int threads, u64 items) {
 }
 
 template <int LOGN>
-int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64* dst, u32 polys, u64 pstride,
-                 u32 limb0, u32 nlimbs, hipStream_t s) {
+int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* dst,
+                 u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
   using G = Geo<LOGN>;
   const u64 pl = (u64)polys * nlimbs;
-  const PolyMap pm = flat_map(pstride);
+  const PolyMap pm{1, spstride, 0, dpstride, 0, 0};
+  // the second pass runs in place on dst
+  const PolyMap pd = flat_map(dpstride);
   const u64 ic = pl * G::TILES_C, ir = pl * G::TILES_R;
   if (fwd) {
     k_ntt_col<LOGN, true><<<item_grid<k_ntt_col<LOGN, true>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
-        src, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd, c->d_nfold, c->d_mods);
+        src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd, c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_fwd");
     k_ntt_row<LOGN, true><<<item_grid<k_ntt_row<LOGN, true>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
-        dst, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_fwd, c->d_mods);
+        dst, dst, nlimbs, limb0, pd, (u32)ir, c->d_tw_fwd, c->d_mods);
     prof_mark(s, "ntt_row_fwd");
   } else {
     k_ntt_row<LOGN, false><<<item_grid<k_ntt_row<LOGN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
         src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv, c->d_mods);
     prof_mark(s, "ntt_row_inv");
     k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
-        dst, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_inv, c->d_nfold, c->d_mods);
+        dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv, c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_inv");
   }
   FHE_HIP_CHECK(hipGetLastError());
@@ -818,16 +843,14 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   using H = HmGeo<LOGN>;
   constexpr u64 N = 1ull << LOGN;
   const u64 limbN = (u64)nlimbs * N;
-  // x: [batch][4][nlimbs][N] workspace; A0, A1 -> slots 0, 1; B0, B1 -> slots 2, 3.
-  const PolyMap to_x{2, 2 * limbN, limbN, 4 * limbN, limbN};
-  const u64 ic = (u64)batch * 2 * nlimbs * G::TILES_C;
-  const dim3 gc = item_grid<k_ntt_col<LOGN, true>, kLoopCol>(c, G::THR_C, ic);
-  k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(a, x, nlimbs, limb0, to_x, (u32)ic, c->d_tw_fwd,
-                                               c->d_nfold, c->d_mods);
-  prof_mark(s, "hm_col_fwd_a");
-  k_ntt_col<LOGN, true><<<gc, G::THR_C, 0, s>>>(b, x + 2 * limbN, nlimbs, limb0, to_x, (u32)ic,
-                                               c->d_tw_fwd, c->d_nfold, c->d_mods);
-  prof_mark(s, "hm_col_fwd_b");
+  // x: [batch][4][nlimbs][N] workspace; A0, A1 -> slots 0, 1; B0, B1 -> slots 2, 3: one launch
+  // over the 4 polys of every ciphertext pair (group of 4: slots 0, 1 from a, slots 2, 3 from b)
+  const PolyMap to_x{4, 2 * limbN, limbN, 4 * limbN, limbN, 2};
+  const u64 ic = (u64)batch * 4 * nlimbs * G::TILES_C;
+  k_ntt_col<LOGN, true><<<item_grid<k_ntt_col<LOGN, true>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0,
+                          s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic, c->d_tw_fwd, c->d_nfold,
+                               c->d_mods);
+  prof_mark(s, "hm_col_fwd");
   const dim3 gh((u32)((u64)batch * nlimbs * H::TILES));
   k_hommult_row<LOGN><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd, c->d_tw_inv,
                                             c->d_mods);
@@ -835,7 +858,8 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
   k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, kLoopCol>(c, G::THR_C, ii), G::THR_C, 0, s>>>(
-      d, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv, c->d_nfold + 2, c->d_mods);
+      d, nullptr, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv, c->d_nfold + 2,
+      c->d_mods);
   prof_mark(s, "hm_col_inv");
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;
@@ -847,11 +871,16 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
 
 int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 polys, u64 pstride,
                u32 limb0, u32 nlimbs, hipStream_t s) {
+  return launch_ntt_strided(c, forward, src, pstride, dst, pstride, polys, limb0, nlimbs, s);
+}
+
+int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
+                       u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
   if ((u64)polys * nlimbs == 0) return kOk;
   switch (c->log_n) {
 #define X(n) \
   case n:    \
-    return ntt_dispatch<n>(c, forward, src, dst, polys, pstride, limb0, nlimbs, s);
+    return ntt_dispatch<n>(c, forward, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
     FHE_LOGN_CASES(X)
 #undef X
   }

@@ -70,68 +70,70 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
 }
 
 // acc{0,1}[b][r][i] = sum_j e_j[b][r][i] * evk{b,a}[j][r][i] mod t over own Q-limbs then P-limbs;
-// e_j = d2_own row when row r's limb is in digit j, else ext[j][b] row (NTT form).  Each thread
-// owns one (r, i), holds its 2 * dnum evaluation-key words in registers and walks the batch, so
-// the key -- the dominant traffic of a key-switch -- is read once per batch.
+// e_j = d2_own row when row r's limb is in digit j, else ext[j][b] row (NTT form).  Grid: x over
+// coefficients, y = row r (limb and modulus uniform per workgroup).  Each thread holds its
+// 2 DNUM evaluation-key words in registers and walks the batch, so the key -- the dominant
+// traffic of a key-switch -- is read once per batch; the DNUM products of a sum are accumulated
+// as 128-bit integers (< 16 q^2) and reduced once (reduce128).
 constexpr int kMaxDnum = 16;
+template <int DNUM>
 __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc, u64 acc_ws,
                                                        const u64* __restrict__ ext,
                                                        const u64* __restrict__ d2_own,
                                                        const u64* __restrict__ evk_b,
                                                        const u64* __restrict__ evk_a, u32 rows,
-                                                       u32 nq, RowMap map, u32 dnum, u32 alpha,
-                                                       u32 L, u32 batch, u64 n,
+                                                       u32 nq, RowMap map, u32 alpha, u32 L,
+                                                       u32 batch, u32 log_n,
                                                        const ModParams* __restrict__ mods) {
-  const u64 total = (u64)rows * n;
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  const u64 rn = (u64)rows * n;
-  for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const u32 r = (u32)(e / n);
-    const u64 i = e % n;
-    const u32 limb = map.limb(r);
-    const ModParams m = mods[limb];
-    const u32 own_digit = limb < L ? limb / alpha : 0xffffffffu;
-    u64 kb[kMaxDnum], ka[kMaxDnum];
-    for (u32 j = 0; j < dnum; ++j) {
-      kb[j] = evk_b[(u64)j * rn + e];
-      ka[j] = evk_a[(u64)j * rn + e];
+  const u32 r = blockIdx.y;
+  const u64 n = 1ull << log_n, rn = (u64)rows * n;
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u64 e = (u64)r * n + i;
+  const u32 limb = map.limb(r);
+  const ModParams m = mods[limb];
+  const u32 own = limb < L ? limb / alpha : 0xffffffffu;
+  u64 kb[DNUM], ka[DNUM];
+#pragma unroll
+  for (int j = 0; j < DNUM; ++j) {
+    kb[j] = evk_b[(u64)j * rn + e];
+    ka[j] = evk_a[(u64)j * rn + e];
+  }
+  for (u32 b = 0; b < batch; ++b) {
+    u128 s0 = 0, s1 = 0;
+#pragma unroll
+    for (int j = 0; j < DNUM; ++j) {
+      const u64 x = (u32)j == own ? d2_own[((u64)b * nq + r) * n + i]
+                                  : ext[((u64)j * batch + b) * rn + e];
+      s0 += (u128)x * kb[j];
+      s1 += (u128)x * ka[j];
     }
-    for (u32 b = 0; b < batch; ++b) {
-      u64 s0 = 0, s1 = 0;
-      for (u32 j = 0; j < dnum; ++j) {
-        const u64 x = j == own_digit ? d2_own[((u64)b * nq + r) * n + i]
-                                     : ext[((u64)j * batch + b) * rn + e];
-        s0 = csub(s0 + mulmod_barrett(x, kb[j], m), m.q);
-        s1 = csub(s1 + mulmod_barrett(x, ka[j], m), m.q);
-      }
-      acc[(u64)b * rn + e] = s0;
-      acc[acc_ws + (u64)b * rn + e] = s1;
-    }
+    acc[(u64)b * rn + e] = reduce128((u64)s0, (u64)(s0 >> 64), m);
+    acc[acc_ws + (u64)b * rn + e] = reduce128((u64)s1, (u64)(s1 >> 64), m);
   }
 }
 
 // out{0,1}[b][r][i] = (acc{0,1}[b][r][i] - conv{0,1}[b][r][i]) * P^-1 mod q over own Q-limbs.
+// Grid: x over coefficients, y = own Q-limb r, z = batch entry b.
 __global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ out0,
                                                              u64* __restrict__ out1,
                                                              const u64* __restrict__ acc,
                                                              u64 acc_ws, u32 rows,
                                                              const u64* __restrict__ conv,
-                                                             u32 nq, u32 limb0, u32 batch, u64 n,
+                                                             u32 nq, u32 limb0, u32 log_n,
                                                              const ulonglong2* __restrict__ pinv,
                                                              const ModParams* __restrict__ mods) {
-  const u64 per = (u64)nq * n;
-  const u64 total = (u64)batch * per;
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const u64 b = e / per, ri = e % per;
-    const u32 limb = limb0 + (u32)(ri / n);
-    const u64 q = mods[limb].q;
-    const ulonglong2 w = pinv[limb];
-    const u64 ai = b * (u64)rows * n + ri;  // acc rows [0, nq) are the own Q-limbs
-    const u64 c0 = conv[e], c1 = conv[total + e];
-    out0[e] = csub(shoup_lazy(acc[ai] + q - c0, w.x, w.y, q), q);
-    out1[e] = csub(shoup_lazy(acc[acc_ws + ai] + q - c1, w.x, w.y, q), q);
-  }
+  const u64 n = 1ull << log_n;
+  const u32 r = blockIdx.y, b = blockIdx.z;
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 limb = limb0 + r;
+  const u64 q = mods[limb].q;
+  const ulonglong2 w = pinv[limb];
+  const u64 total = (u64)gridDim.z * nq * n;
+  const u64 e = ((u64)b * nq + r) * n + i;
+  const u64 ai = ((u64)b * rows + r) * n + i;  // acc rows [0, nq) are the own Q-limbs
+  const u64 c0 = conv[e], c1 = conv[total + e];
+  out0[e] = csub(shoup_lazy(acc[ai] + q - c0, w.x, w.y, q), q);
+  out1[e] = csub(shoup_lazy(acc[acc_ws + ai] + q - c1, w.x, w.y, q), q);
 }
 
 template <class T>
@@ -284,8 +286,17 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
     u64* ep = e + (u64)nlimbs * n;
     if ((rc = launch_ntt(c, true, ep, ep, batch, rn, L, K, s))) return rc;
   }
-  k_ks_inner<<<grid_for(rn), kThreads, 0, s>>>(acc, acc_ws, ext, d2_own, evk_b, evk_a, rows,
-                                               nlimbs, map, c->dnum, alpha, L, batch, n, c->d_mods);
+  prof_mark(s, "ks_modup");
+  const dim3 gi((u32)(n / kThreads), rows);
+  switch (c->dnum) {
+#define X(k)                                                                                     \
+  case k:                                                                                        \
+    k_ks_inner<k><<<gi, kThreads, 0, s>>>(acc, acc_ws, ext, d2_own, evk_b, evk_a, rows, nlimbs, \
+                                          map, alpha, L, batch, c->log_n, c->d_mods);           \
+    break;
+    X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+#undef X
+  }
   FHE_HIP_CHECK(hipGetLastError());
   prof_mark(s, "ks_inner");
   // ModDown: INTT the P rows of both accumulators, convert P -> own Q-limbs, NTT, finish
@@ -295,10 +306,11 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
                     2 * batch};
   if ((rc = baseconv_any(K, down, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, s)))
     return rc;
+  prof_mark(s, "ks_moddown_conv");
   if ((rc = launch_ntt(c, true, conv, conv, 2 * batch, (u64)nlimbs * n, limb0, nlimbs, s)))
     return rc;
-  k_moddown_finish<<<grid_for(B * nlimbs * n), kThreads, 0, s>>>(
-      ks0, ks1, acc, acc_ws, rows, conv, nlimbs, limb0, batch, n, c->d_pinv, c->d_mods);
+  k_moddown_finish<<<dim3((u32)(n / kThreads), nlimbs, batch), kThreads, 0, s>>>(
+      ks0, ks1, acc, acc_ws, rows, conv, nlimbs, limb0, c->log_n, c->d_pinv, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
   prof_mark(s, "moddown_finish");
   return kOk;

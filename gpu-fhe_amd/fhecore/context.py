@@ -67,7 +67,7 @@ def to_host(t) -> np.ndarray:
 
 
 def _ptr(t) -> int:
-    return ctypes.c_void_p(t.data_ptr())
+    return ctypes.c_void_p(t.data_ptr() if t is not None else None)
 
 
 def _stream(t):
@@ -234,6 +234,56 @@ class Context:
             check(lib.fhe_keyswitch(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(d2), _ptr(evk_b),
                                     _ptr(evk_a), batch, _ptr(ws), _stream(d2)), "fhe_keyswitch")
         return ks0, ks1
+
+    # ---- rescale and rotation -------------------------------------
+    def galois_elt(self, step: int) -> int:
+        """Galois element of a slot rotation by `step` (5^step mod 2N; negative steps invert)."""
+        two_n = 2 * self.n
+        return pow(5, step, two_n) if step >= 0 else pow(pow(5, -step, two_n), -1, two_n)
+
+    def rescale(self, x, ntt_form: bool = True, workspace=None):
+        """Divide-and-round by the last modulus: x [..., l, N] over Q-limbs 0..l-1 (2 <= l <= L)
+        -> [..., l - 1, N], same form (oracle: pyoracle.rescale_ntt/_coeff)."""
+        _check_tensor(x, "x", (self.n,))
+        nl = x.shape[-2]
+        polys = x.numel() // (nl * self.n)
+        out = torch.empty(*x.shape[:-2], nl - 1, self.n, dtype=x.dtype, device=x.device)
+        lib = load()
+        ws = None
+        if ntt_form:
+            ws = workspace if workspace is not None else self.workspace(
+                lib.fhe_rescale_workspace(self._ptr, polys, nl))
+        with torch.cuda.device(self.device):
+            check(lib.fhe_rescale(self._ptr, _ptr(out), _ptr(x), polys, nl, int(ntt_form),
+                                  _ptr(ws), _stream(x)), "fhe_rescale")
+        return out
+
+    def automorphism(self, x, galois_elt: int, ntt_form: bool = True, limb0: int = 0):
+        """sigma_k(a)(X) = a(X^k) on x [..., nlimbs, N] over limbs [limb0, limb0 + nlimbs)."""
+        _check_tensor(x, "x", (self.n,))
+        nl = x.shape[-2]
+        polys = x.numel() // (nl * self.n)
+        out = torch.empty_like(x)
+        with torch.cuda.device(self.device):
+            check(load().fhe_automorphism(self._ptr, _ptr(out), _ptr(x), polys, limb0, nl,
+                                          galois_elt, int(ntt_form), _stream(x)), "fhe_automorphism")
+        return out
+
+    def rotate(self, ct, galois_elt: int, rot_b, rot_a, workspace=None):
+        """ct [..., 2, L, N] NTT form -> (sigma c0 + KS0(sigma c1), KS1(sigma c1)) with the
+        key-switch key rot_b/rot_a [dnum, L + K, N] from sigma_k(s) to s."""
+        _check_tensor(ct, "ct", (2, self.L, self.n))
+        if tuple(rot_b.shape) != (self.dnum, self.L + self.K, self.n) or rot_a.shape != rot_b.shape:
+            raise ValueError("rotate: key must be [dnum, L + K, N]")
+        batch = ct.numel() // (2 * self.L * self.n)
+        out = torch.empty_like(ct)
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_rotate_workspace(self._ptr, batch))
+        with torch.cuda.device(self.device):
+            check(lib.fhe_rotate(self._ptr, _ptr(out), _ptr(ct), galois_elt, _ptr(rot_b),
+                                 _ptr(rot_a), batch, _ptr(ws), _stream(ct)), "fhe_rotate")
+        return out
 
     def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0: int, workspace=None):
         """One rank's key-switch (see fhecore.dist): c_all [..., L, N] coefficient form,

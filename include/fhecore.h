@@ -134,6 +134,31 @@ int fhe_keyswitch_shard(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const 
                         uint32_t limb0, uint32_t nlimbs, uint32_t batch, void* workspace,
                         fhe_stream_t stream);
 
+/* ---- rescale and rotation (not in the reference) ---------------------
+ * Standard RNS-CKKS operations on this library's layout, restated by oracle/pyoracle.py
+ * (rescale_coeff / rescale_ntt, automorphism_*, rotate).
+ * fhe_rescale: divide-and-round by the last modulus.  in [polys][nlimbs][N] over Q-limbs
+ * 0 .. nlimbs-1 (2 <= nlimbs <= L) -> out [polys][nlimbs-1][N], out_i = floor((X + q_l/2) / q_l)
+ * mod q_i for the CRT value X; ntt_form selects NTT or coefficient form for both (the NTT form
+ * needs a workspace of fhe_rescale_workspace bytes; NULL = internal). */
+size_t fhe_rescale_workspace(const fhe_ctx* ctx, uint32_t polys, uint32_t nlimbs);
+int fhe_rescale(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t polys,
+                uint32_t nlimbs, int ntt_form, void* workspace, fhe_stream_t stream);
+/* fhe_automorphism: sigma_k(a)(X) = a(X^k) for an odd Galois element k < 2N, on
+ * [polys][nlimbs][N] rows over limbs [limb0, limb0 + nlimbs), NTT or coefficient form (a slot
+ * permutation, resp. a signed coefficient permutation).  out must not alias in.  Rotating the
+ * slots by r uses k = 5^r mod 2N, conjugation k = 2N - 1. */
+int fhe_automorphism(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t polys,
+                     uint32_t limb0, uint32_t nlimbs, uint32_t galois_elt, int ntt_form,
+                     fhe_stream_t stream);
+/* fhe_rotate: in, out [batch][2][L][N] NTT form over Q (out must not alias in);
+ * out = (sigma_k c0 + KS0(sigma_k c1), KS1(sigma_k c1)) with rot_b, rot_a [dnum][L + K][N] the
+ * key-switch key from sigma_k(s) to s (NTT form, as for fhe_keyswitch). */
+size_t fhe_rotate_workspace(const fhe_ctx* ctx, uint32_t batch);
+int fhe_rotate(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t galois_elt,
+               const uint64_t* rot_b, const uint64_t* rot_a, uint32_t batch, void* workspace,
+               fhe_stream_t stream);
+
 /* ---- timing marks (measurement support, not part of the reference surface) ------------------
  * fhe_prof_begin records a HIP event on `stream`, then every kernel this host thread launches
  * through libfhecore records one more event after itself (up to max_marks).  fhe_prof_end waits

@@ -169,6 +169,40 @@ class Evaluator {
           "fhe_keyswitch");
     return {std::move(k0), std::move(k1)};
   }
+  // Divide-and-round by the last modulus: drops one limb, keeps the form.
+  Ciphertext rescale(const Ciphertext& x) const {
+    if (x.limbs < 2) throw Error(FHE_EINVAL, "rescale: need at least 2 limbs");
+    Ciphertext out(ctx_, x.components, x.limbs - 1, x.ntt_form);
+    const size_t need = fhe_rescale_workspace(ctx_.get(), x.components, x.limbs);
+    if (x.ntt_form && ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
+    check(fhe_rescale(ctx_.get(), out.data(), x.data(), x.components, x.limbs, x.ntt_form ? 1 : 0,
+                      x.ntt_form ? ws_.data() : nullptr, s_),
+          "fhe_rescale");
+    return out;
+  }
+  // Galois element of a slot rotation by `step` (5^step mod 2N).
+  uint32_t galois_elt(int step) const {
+    const uint64_t two_n = 2 * ctx_.n();
+    uint64_t g = 1, b = 5;
+    uint64_t e = step >= 0 ? (uint64_t)step : (uint64_t)(-(int64_t)step) * (two_n / 2 - 1);
+    for (; e; e >>= 1, b = b * b % two_n)
+      if (e & 1) g = g * b % two_n;
+    return (uint32_t)g;
+  }
+  // Rotation of a 2-component NTT-form ciphertext over all L limbs by Galois element k, with the
+  // key-switch key from sigma_k(s) to s (NTT form [dnum][L+K][N]).
+  Ciphertext rotate(const Ciphertext& ct, uint32_t galois_elt, const DeviceBuffer& rot_b,
+                    const DeviceBuffer& rot_a) const {
+    if (ct.components != 2 || !ct.ntt_form || ct.limbs != ctx_.L())
+      throw Error(FHE_EINVAL, "rotate: need a 2-component NTT-form ciphertext over L limbs");
+    Ciphertext out(ctx_, 2, ct.limbs, true);
+    const size_t need = fhe_rotate_workspace(ctx_.get(), 1);
+    if (ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
+    check(fhe_rotate(ctx_.get(), out.data(), ct.data(), galois_elt, rot_b.data(), rot_a.data(), 1,
+                     ws_.data(), s_),
+          "fhe_rotate");
+    return out;
+  }
 
  private:
   static void same(const Ciphertext& a, const Ciphertext& b, const char* who) {

@@ -490,3 +490,128 @@ def keyswitch_shard(c_all, d2_own, evk_b_own, evk_a_own, qs, ps, dnum, lo, hi):
         outs.append(np.stack([(acc[i] - conv[i]) * pow(P % q, -1, q) % q
                               for i, q in enumerate(qs[lo:hi])]))
     return outs[0], outs[1]
+
+
+# ---- rescale and rotation (Galois automorphisms) ------------------------
+# Not in the reference (its repo has no ciphertext operations beyond poly_add); restated from the
+# standard RNS-CKKS definitions (SEAL's divide_and_round_q_last / apply_galois, OpenFHE's
+# ModReduce / Automorphism), on this repo's layout and NTT convention (SURVEY.md §8a').
+
+
+def galois_elt(step: int, n: int) -> int:
+    """Galois element of a rotation by `step` slots: 5^step mod 2N (step < 0: 5^-|step|)."""
+    return pow(5, step, 2 * n) if step >= 0 else pow(pow(5, -step, 2 * n), -1, 2 * n)
+
+
+def automorphism_coeff(x, k: int, moduli):
+    """sigma_k(a)(X) = a(X^k), k odd, coefficient form (L, N): coefficient i moves to i k mod 2N,
+    negated when that lands in [N, 2N)."""
+    x = np.asarray(x, dtype=object)
+    n = x.shape[-1]
+    out = np.zeros_like(x)
+    for l, q in enumerate(moduli):
+        q = int(q)
+        for i in range(n):
+            m = i * k % (2 * n)
+            v = int(x[l][i])
+            if m < n:
+                out[l][m] = v
+            else:
+                out[l][m - n] = (q - v) % q
+    return out
+
+
+def automorphism_ntt_index(k: int, log_n: int):
+    """NTT-domain automorphism as a gather: out[j] = in[src[j]].  Slot j holds the evaluation at
+    psi^(2 brv(j) + 1); sigma_k maps it to the evaluation at psi^((2 brv(j) + 1) k)."""
+    n = 1 << log_n
+    src = []
+    for j in range(n):
+        e = (2 * bitrev(j, log_n) + 1) * k % (2 * n)
+        src.append(bitrev((e - 1) // 2, log_n))
+    return src
+
+
+def automorphism_ntt(x, k: int, log_n: int):
+    idx = automorphism_ntt_index(k, log_n)
+    x = np.asarray(x, dtype=object)
+    return x[..., idx]
+
+
+def gen_switch_key(s, s_from_ntt, qs, ps, dnum, rng):
+    """Key-switch key from s_from (given in NTT form over Q u P) to s: the gen_relin_key
+    construction with s^2 replaced by s_from (evk_j = (-a_j s + e_j + P g_j s_from, a_j))."""
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    allm = qs + ps
+    n = len(s)
+    Q, P = math.prod(qs), math.prod(ps)
+    s_n = rns_ntt_fwd(_to_rns(s, allm), allm)
+    mods = _mods_col(allm)
+    evk_b, evk_a = [], []
+    for lo, hi in digit_ranges(len(qs), dnum):
+        Dj = math.prod(qs[lo:hi])
+        Qhat = Q // Dj
+        g = Qhat * pow(Qhat % Dj, -1, Dj)
+        a = np.stack([np.array([rng.randrange(m) for _ in range(n)], dtype=object) for m in allm])
+        e = [rng.randrange(-3, 4) for _ in range(n)]
+        e_n = rns_ntt_fwd(_to_rns(e, allm), allm)
+        pg = np.array([(P * g) % m for m in allm], dtype=object).reshape(-1, 1)
+        b = (-a * s_n + e_n + pg * np.asarray(s_from_ntt, dtype=object)) % mods
+        evk_b.append(b)
+        evk_a.append(a)
+    return np.stack(evk_b), np.stack(evk_a)
+
+
+def gen_rot_key(s, k: int, qs, ps, dnum, rng):
+    """Rotation key for Galois element k: switches sigma_k(s) back to s."""
+    allm = [int(m) for m in list(qs) + list(ps)]
+    sk = automorphism_coeff(_to_rns(s, allm), k, allm)
+    return gen_switch_key(s, rns_ntt_fwd(sk, allm), qs, ps, dnum, rng)
+
+
+def rotate(ct_ntt, k: int, rot_b, rot_a, qs, ps, dnum, log_n: int):
+    """ct = (c0, c1) in NTT form over Q: (sigma_k c0 + KS0(sigma_k c1), KS1(sigma_k c1)).
+    Decrypts to sigma_k(m) under s."""
+    c0 = automorphism_ntt(ct_ntt[0], k, log_n)
+    c1 = automorphism_ntt(ct_ntt[1], k, log_n)
+    ks0, ks1 = keyswitch(c1, rot_b, rot_a, qs, ps, dnum)
+    col = _mods_col(qs)
+    return np.stack([(c0 + ks0) % col, ks1 % col])
+
+
+def rescale_coeff(x, moduli):
+    """Divide-and-round by the last modulus: x (l, N) coefficient form over q_0..q_{l-1} ->
+    (l - 1, N) with out_i = floor((X + q_last // 2) / q_last) mod q_i, X the CRT value in
+    [0, Q).  RNS form: (x_i - ((x_last + h) mod q_last - h)) q_last^-1 mod q_i, h = q_last // 2."""
+    moduli = [int(q) for q in moduli]
+    x = np.asarray(x, dtype=object)
+    ql = moduli[-1]
+    h = ql // 2
+    t = (x[-1] + h) % ql
+    out = []
+    for i, q in enumerate(moduli[:-1]):
+        tmp = (t - h) % q
+        out.append((x[i] - tmp) * pow(ql % q, -1, q) % q)
+    return np.stack(out)
+
+
+def rescale_exact(x, moduli):
+    """The same through CRT big integers (test cross-check of rescale_coeff)."""
+    moduli = [int(q) for q in moduli]
+    Q = math.prod(moduli)
+    x = np.asarray(x, dtype=object)
+    X = 0
+    for i, q in enumerate(moduli):
+        hat = Q // q
+        X = X + x[i] * (hat * pow(hat % q, -1, q))
+    X = X % Q
+    ql = moduli[-1]
+    Y = (X + ql // 2) // ql
+    return np.stack([Y % q for q in moduli[:-1]])
+
+
+def rescale_ntt(x, moduli):
+    """Rescale of an NTT-form (l, N) input: INTT, divide-and-round, NTT over the l - 1 limbs."""
+    c = rns_ntt_inv(x, moduli)
+    return rns_ntt_fwd(rescale_coeff(c, moduli), moduli[:-1])

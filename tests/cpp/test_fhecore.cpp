@@ -64,6 +64,35 @@ int main() {
       std::printf("FAIL ntt round trip\n");
       return 1;
     }
+    // rescale (coefficient form) of d = (d0, d1, d2) over 2 limbs: X = CRT(x0, x1) < q0 q1 < 2^122,
+    // out = floor((X + q1 / 2) / q1) mod q0
+    {
+      fhe::Ciphertext dc = ev.rescale(d);
+      if (dc.limbs != 1) {
+        std::printf("FAIL rescale shape\n");
+        return 1;
+      }
+      const std::vector<u64> hr = dc.buf.download();
+      const u64 q0 = q[0], q1 = q[1];
+      const u64 q0inv_mod_q1 = [&] {  // q0^-1 mod q1 by Fermat
+        u128 r = 1, b = q0 % q1;
+        for (u64 e = q1 - 2; e; e >>= 1, b = b * b % q1)
+          if (e & 1) r = r * b % q1;
+        return (u64)r;
+      }();
+      for (uint32_t c = 0; c < 3; ++c)
+        for (u64 i = 0; i < n; ++i) {
+          const u64 x0 = hd[(c * L + 0) * n + i], x1 = hd[(c * L + 1) * n + i];
+          // X = x0 + q0 * ((x1 - x0) q0^-1 mod q1)
+          const u64 t = (u64)((u128)((x1 + q1 - x0 % q1) % q1) * q0inv_mod_q1 % q1);
+          const u128 X = (u128)x0 + (u128)q0 * t;
+          const u64 want = (u64)(((X + q1 / 2) / q1) % q0);
+          if (hr[c * n + i] != want) {
+            std::printf("FAIL rescale comp %u coeff %llu\n", c, (unsigned long long)i);
+            return 1;
+          }
+        }
+    }
     std::printf("cpp api ok\n");
     return 0;
   } catch (const fhe::Error& e) {

@@ -64,8 +64,9 @@ def test_mont_reduce_lazy(q):
     R_inv = pow(1 << 64, -1, q)
     cases = [0, 1, q * q - 1, 2 * q * q - 1, q << 64 - 1]
     cases += [rng.randrange(q) * rng.randrange(q) for _ in range(2000)]
-    cases += [rng.randrange(q) * rng.randrange(q) + rng.randrange(q) * rng.randrange(q)
-              for _ in range(2000)]  # d1 = a0 b1 + a1 b0 < 2 q^2
+    cases += [rng.randrange(2 * q) * rng.randrange(2 * q) + rng.randrange(2 * q) * rng.randrange(2 * q)
+              for _ in range(2000)]  # d1 = a0 b1 + a1 b0 with lazy operands < 2q: below 8 q^2
+    cases += [8 * q * q - 1]
     for t in cases:
         r = mont_reduce_lazy(t, q)
         assert 0 <= r < 2 * q, t

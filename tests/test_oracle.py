@@ -149,3 +149,64 @@ def test_keyswitch_decrypts_with_real_keys():
     err = (ks0.astype(object) + ks1.astype(object) * sn - d2 * sn * sn) % col
     e = pyoracle.crt_centered(pyoracle.rns_ntt_inv(err, qs), qs)
     assert max(abs(int(v)) for v in e) < 1 << 20
+
+
+# ---- rescale / automorphism / rotation (oracle self-consistency) -----
+
+def test_automorphism_coeff_matches_ntt_gather():
+    log_n = 6
+    n = 1 << log_n
+    qs = pyoracle.gen_moduli(log_n, 2)
+    rng = random.Random(5)
+    x = np.stack([np.array([rng.randrange(q) for _ in range(n)], dtype=object) for q in qs])
+    for k in (pyoracle.galois_elt(1, n), pyoracle.galois_elt(-3, n), 2 * n - 1):
+        a = pyoracle.rns_ntt_fwd(pyoracle.automorphism_coeff(x, k, qs), qs)
+        b = pyoracle.automorphism_ntt(pyoracle.rns_ntt_fwd(x, qs), k, log_n)
+        assert (a == b).all()
+
+
+def test_automorphism_is_ring_homomorphism():
+    """sigma_k(a b) = sigma_k(a) sigma_k(b) (negacyclic products)."""
+    log_n = 5
+    n = 1 << log_n
+    q = pyoracle.gen_moduli(log_n, 1)[0]
+    rng = random.Random(6)
+    a = [rng.randrange(q) for _ in range(n)]
+    b = [rng.randrange(q) for _ in range(n)]
+    k = pyoracle.galois_elt(2, n)
+    s = lambda v: list(pyoracle.automorphism_coeff(np.array([v], dtype=object), k, [q])[0])  # noqa: E731
+    assert s(pyoracle.negacyclic_mul(a, b, q)) == list(pyoracle.negacyclic_mul(s(a), s(b), q))
+
+
+@pytest.mark.parametrize("L", [2, 3, 5])
+def test_rescale_rns_formula_is_exact_divide_and_round(L):
+    log_n = 5
+    qs = pyoracle.gen_moduli(log_n, L)
+    rng = random.Random(L)
+    x = np.stack([np.array([rng.randrange(q) for _ in range(1 << log_n)], dtype=object) for q in qs])
+    assert (pyoracle.rescale_coeff(x, qs) == pyoracle.rescale_exact(x, qs)).all()
+
+
+def test_rotation_decrypts_to_rotated_message():
+    """Encrypt m, rotate with a real rotation key, decrypt: sigma_k(m) + small noise."""
+    log_n, L, K, dnum = 5, 3, 2, 3
+    n = 1 << log_n
+    mods = pyoracle.gen_moduli(log_n, L + K)
+    qs, ps = mods[:L], mods[L:]
+    rng = random.Random(21)
+    s = [rng.randrange(-1, 2) for _ in range(n)]
+    m = [rng.randrange(-1000, 1000) for _ in range(n)]
+    col = pyoracle._mods_col(qs)
+    s_n = pyoracle.rns_ntt_fwd(pyoracle._to_rns(s, qs), qs)
+    a = np.stack([np.array([rng.randrange(q) for _ in range(n)], dtype=object) for q in qs])
+    e = pyoracle.rns_ntt_fwd(pyoracle._to_rns([rng.randrange(-3, 4) for _ in range(n)], qs), qs)
+    m_n = pyoracle.rns_ntt_fwd(pyoracle._to_rns(m, qs), qs)
+    ct = np.stack([(-a * s_n + e + m_n) % col, a])
+    k = pyoracle.galois_elt(1, n)
+    rb, ra = pyoracle.gen_rot_key(s, k, qs, ps, dnum, rng)
+    out = pyoracle.rotate(ct, k, rb, ra, qs, ps, dnum, log_n)
+    dec = pyoracle.crt_centered(pyoracle.rns_ntt_inv((out[0] + out[1] * s_n) % col, qs), qs)
+    want = pyoracle.automorphism_coeff(np.array([[v % qs[0] for v in m]], dtype=object), k,
+                                       [qs[0]])[0]
+    want = [int(v) - qs[0] if int(v) > qs[0] // 2 else int(v) for v in want]
+    assert max(abs(int(d) - w) for d, w in zip(dec, want)) < 1 << 20
