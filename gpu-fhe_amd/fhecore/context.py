@@ -285,6 +285,34 @@ class Context:
                                  _ptr(rot_a), batch, _ptr(ws), _stream(ct)), "fhe_rotate")
         return out
 
+    # ---- wire format ----------------------------------------------
+    def serialize(self, x, ntt_form: bool, limb0: int = 0) -> bytes:
+        """x [..., nlimbs, N] over limbs [limb0, limb0 + nlimbs) -> an FHEC v1 blob."""
+        _check_tensor(x, "x", (self.n,))
+        nl = x.shape[-2]
+        polys = x.numel() // (nl * self.n)
+        lib = load()
+        size = lib.fhe_serialized_size(self._ptr, polys, nl)
+        buf = ctypes.create_string_buffer(size)
+        with torch.cuda.device(self.device):
+            check(lib.fhe_serialize(self._ptr, _ptr(x), polys, limb0, nl, int(ntt_form), buf, size,
+                                    _stream(x)), "fhe_serialize")
+        return buf.raw
+
+    def deserialize(self, blob: bytes):
+        """FHEC v1 blob -> (tensor [polys, nlimbs, N] on this context's device, limb0, ntt_form).
+        Rejects blobs for another N / other moduli, corrupted or out-of-range data."""
+        lib = load()
+        polys, limb0, nl, ntt = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+        check(lib.fhe_deserialize(self._ptr, blob, len(blob), None, 0, ctypes.byref(polys),
+                                  ctypes.byref(limb0), ctypes.byref(nl), ctypes.byref(ntt), None),
+              "fhe_deserialize")
+        out = torch.empty(polys.value, nl.value, self.n, dtype=torch.int64, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(lib.fhe_deserialize(self._ptr, blob, len(blob), _ptr(out), out.numel(), None, None,
+                                      None, None, _stream(out)), "fhe_deserialize")
+        return out, limb0.value, bool(ntt.value)
+
     def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0: int, workspace=None):
         """One rank's key-switch (see fhecore.dist): c_all [..., L, N] coefficient form,
         d2_own [..., nlimbs, N] NTT form, evk slices [dnum, nlimbs + K, N]."""

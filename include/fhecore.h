@@ -159,6 +159,22 @@ int fhe_rotate(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t g
                const uint64_t* rot_b, const uint64_t* rot_a, uint32_t batch, void* workspace,
                fhe_stream_t stream);
 
+/* ---- wire format (not in the reference) ------------------------------
+ * A self-describing little-endian blob for any [polys][nlimbs][N] residue tensor over context
+ * limbs [limb0, limb0 + nlimbs) -- ciphertexts, keys, plaintexts: "FHEC", version 1, flags (bit 0
+ * NTT form), log_n, polys, limb0, nlimbs, the nlimbs moduli, the residues, an FNV-1a-64 checksum
+ * (layout in gpu-fhe_amd/csrc/serialize.cpp).  fhe_serialize copies device -> host and
+ * synchronises `stream`.  fhe_deserialize validates the blob against the context (N, moduli,
+ * checksum, every residue below its modulus) before copying host -> device; with dev == NULL it
+ * only validates and reports the shape, so a caller can size the device buffer (dev_words). */
+size_t fhe_serialized_size(const fhe_ctx* ctx, uint32_t polys, uint32_t nlimbs);
+int fhe_serialize(const fhe_ctx* ctx, const uint64_t* dev, uint32_t polys, uint32_t limb0,
+                  uint32_t nlimbs, int ntt_form, void* host_buf, size_t buf_size,
+                  fhe_stream_t stream);
+int fhe_deserialize(const fhe_ctx* ctx, const void* host_buf, size_t size, uint64_t* dev,
+                    size_t dev_words, uint32_t* polys, uint32_t* limb0, uint32_t* nlimbs,
+                    int* ntt_form, fhe_stream_t stream);
+
 /* ---- timing marks (measurement support, not part of the reference surface) ------------------
  * fhe_prof_begin records a HIP event on `stream`, then every kernel this host thread launches
  * through libfhecore records one more event after itself (up to max_marks).  fhe_prof_end waits
