@@ -280,4 +280,17 @@ int fhe_rotate(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t gal
   return launch_rotate(c, out, in, galois_elt, rot_b, rot_a, batch, ws, hs(s));
 }
 
+size_t fhe_mul_relin_workspace(const fhe_ctx* c, uint32_t batch) {
+  return c ? mul_relin_workspace_bytes(c, batch) : 0;
+}
+
+int fhe_mul_relin(const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                  const uint64_t* evk_b, const uint64_t* evk_a, uint32_t batch, int rescale,
+                  void* ws, fhe_stream_t s) {
+  int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_mul_relin");
+  if (rc) return rc;
+  if ((rc = ensure_ws(c, mul_relin_workspace_bytes(c, batch), &ws))) return rc;
+  return launch_mul_relin(c, out, a, b, evk_b, evk_a, batch, rescale != 0, ws, hs(s));
+}
+
 }  // extern "C"

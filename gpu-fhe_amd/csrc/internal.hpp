@@ -108,6 +108,11 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
                   const u64* rot_a, u32 batch, void* ws, hipStream_t s);
 size_t rotate_workspace_bytes(const fhe_ctx* c, u32 batch);
 
+// ---- launchers (pipeline.hip): SURVEY.md §8(f) row 4 -----------------------------------
+int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, const u64* evk_b,
+                     const u64* evk_a, u32 batch, bool rescale, void* ws, hipStream_t s);
+size_t mul_relin_workspace_bytes(const fhe_ctx* c, u32 batch);
+
 // ---- host (context.cpp) ----------------------------------------------------------------
 int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 K, u32 dnum,
                int device);

@@ -54,6 +54,12 @@ SIGNATURES = {
     "fhe_serialize": (_i32, [_vp, _vp, _u32, _u32, _u32, _i32, _vp, _sz, _vp]),
     "fhe_deserialize": (_i32, [_vp, _vp, _sz, _vp, _sz, ctypes.POINTER(_u32), ctypes.POINTER(_u32),
                                ctypes.POINTER(_u32), ctypes.POINTER(_i32), _vp]),
+    "fhe_mul_relin_workspace": (_sz, [_vp, _u32]),
+    "fhe_mul_relin": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _i32, _vp, _vp]),
+    "fhe_graph_begin": (_i32, [_vp]),
+    "fhe_graph_end": (_i32, [_vp, ctypes.POINTER(_vp)]),
+    "fhe_graph_launch": (_i32, [_vp, _vp]),
+    "fhe_graph_destroy": (_i32, [_vp]),
     "fhe_prof_begin": (_i32, [_u32, _vp]),
     "fhe_prof_end": (_i32, [ctypes.POINTER(ctypes.c_float), _u32, ctypes.POINTER(_u32),
                             ctypes.c_char_p, _sz]),

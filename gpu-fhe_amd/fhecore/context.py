@@ -285,6 +285,31 @@ class Context:
                                  _ptr(rot_a), batch, _ptr(ws), _stream(ct)), "fhe_rotate")
         return out
 
+    # ---- fused multiply -> relinearise -> rescale ------------------
+    def mul_relin(self, a, b, evk_b, evk_a, rescale: bool = True, workspace=None, out=None):
+        """a, b [..., 2, L, N] NTT form -> Relin(a x b) [..., 2, L, N] (rescale: [..., 2, L-1, N]),
+        NTT form (oracle: pyoracle.mul_relin)."""
+        _check_tensor(a, "a", (2, self.L, self.n))
+        _check_tensor(b, "b", (2, self.L, self.n))
+        if a.shape != b.shape:
+            raise ValueError("mul_relin: a and b must have the same shape")
+        if tuple(evk_b.shape) != (self.dnum, self.L + self.K, self.n) or evk_a.shape != evk_b.shape:
+            raise ValueError("mul_relin: key must be [dnum, L + K, N]")
+        batch = a.numel() // (2 * self.L * self.n)
+        shape = (*a.shape[:-2], self.L - (1 if rescale else 0), self.n)
+        if out is None:
+            out = torch.empty(shape, dtype=a.dtype, device=a.device)
+        elif tuple(out.shape) != shape:
+            raise ValueError(f"mul_relin: out must be {shape}")
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_mul_relin_workspace(self._ptr, batch))
+        with torch.cuda.device(self.device):
+            check(lib.fhe_mul_relin(self._ptr, _ptr(out), _ptr(a), _ptr(b), _ptr(evk_b),
+                                    _ptr(evk_a), batch, int(rescale), _ptr(ws), _stream(a)),
+                  "fhe_mul_relin")
+        return out
+
     # ---- SURVEY.md §8(f) row 2: wire format ----------------------------------------------
     def serialize(self, x, ntt_form: bool, limb0: int = 0) -> bytes:
         """x [..., nlimbs, N] over limbs [limb0, limb0 + nlimbs) -> an FHEC v1 blob."""
@@ -333,3 +358,41 @@ class Context:
                                           _ptr(d2_own), _ptr(evk_b), _ptr(evk_a), limb0, nl,
                                           batch, _ptr(ws), _stream(d2_own)), "fhe_keyswitch_shard")
         return ks0, ks1
+
+
+class Graph:
+    """Capture libfhecore calls issued on the current stream into a HIP graph and replay them
+    (fhe_graph_*).  Every call inside the block needs an explicit (preallocated) workspace or one
+    eager run beforehand; the tensors used are baked into the graph::
+
+        with fhecore.Graph() as g:
+            ctx.mul_relin(a, b, kb, ka, workspace=ws, out=out)
+        g.launch()
+    """
+
+    def __init__(self):
+        self._g = None
+
+    def __enter__(self):
+        self._stream = torch.cuda.current_stream()
+        check(load().fhe_graph_begin(ctypes.c_void_p(self._stream.cuda_stream)), "fhe_graph_begin")
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        g = ctypes.c_void_p()
+        rc = load().fhe_graph_end(ctypes.c_void_p(self._stream.cuda_stream), ctypes.byref(g))
+        if exc_type is None:
+            check(rc, "fhe_graph_end")
+            self._g = g
+        return False
+
+    def launch(self):
+        check(load().fhe_graph_launch(self._g, ctypes.c_void_p(self._stream.cuda_stream)),
+              "fhe_graph_launch")
+
+    def __del__(self):
+        if getattr(self, "_g", None):
+            try:
+                load().fhe_graph_destroy(self._g)
+            except Exception:  # interpreter shutdown
+                pass

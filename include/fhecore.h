@@ -175,6 +175,25 @@ int fhe_deserialize(const fhe_ctx* ctx, const void* host_buf, size_t size, uint6
                     size_t dev_words, uint32_t* polys, uint32_t* limb0, uint32_t* nlimbs,
                     int* ntt_form, fhe_stream_t stream);
 
+/* ---- fused multiply -> relinearise -> rescale ------------------------
+ * a, b [batch][2][L][N] NTT form; evk_b, evk_a [dnum][L + K][N] the relinearisation key (NTT
+ * form, as for fhe_keyswitch).  out = Relin(a x b) [batch][2][L][N], or with rescale != 0 its
+ * divide-and-round by q_{L-1}, [batch][2][L-1][N]; NTT form.  Restated by oracle mul_relin. */
+size_t fhe_mul_relin_workspace(const fhe_ctx* ctx, uint32_t batch);
+int fhe_mul_relin(const fhe_ctx* ctx, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                  const uint64_t* evk_b, const uint64_t* evk_a, uint32_t batch, int rescale,
+                  void* workspace, fhe_stream_t stream);
+
+/* ---- HIP graphs: capture a sequence of libfhecore calls on `stream` and replay it -----------
+ * Between fhe_graph_begin and fhe_graph_end every call must be given an explicit workspace (or
+ * have run once eagerly so the internal one is large enough): nothing may allocate or
+ * synchronise while the stream is capturing.  Replays reuse the captured pointers. */
+typedef struct fhe_graph_s* fhe_graph_t;
+int fhe_graph_begin(fhe_stream_t stream);
+int fhe_graph_end(fhe_stream_t stream, fhe_graph_t* graph);
+int fhe_graph_launch(fhe_graph_t graph, fhe_stream_t stream);
+int fhe_graph_destroy(fhe_graph_t graph);
+
 /* ---- timing marks (measurement support, not part of the reference surface) ------------------
  * fhe_prof_begin records a HIP event on `stream`, then every kernel this host thread launches
  * through libfhecore records one more event after itself (up to max_marks).  fhe_prof_end waits

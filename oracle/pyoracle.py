@@ -615,3 +615,24 @@ def rescale_ntt(x, moduli):
     """Rescale of an NTT-form (l, N) input: INTT, divide-and-round, NTT over the l - 1 limbs."""
     c = rns_ntt_inv(x, moduli)
     return rns_ntt_fwd(rescale_coeff(c, moduli), moduli[:-1])
+
+
+# ---- SURVEY.md §8(f) row 4: the fused multiply -> relinearise -> rescale pipeline ----------------
+
+def tensor_ntt(a, b, moduli):
+    """a, b (2, L, N) NTT form -> (3, L, N): (a0 b0, a0 b1 + a1 b0, a1 b1) mod q per limb."""
+    qs = _mods_col(moduli)
+    a = np.asarray(a, dtype=object)
+    b = np.asarray(b, dtype=object)
+    return np.stack([a[0] * b[0] % qs, (a[0] * b[1] + a[1] * b[0]) % qs, a[1] * b[1] % qs])
+
+
+def mul_relin(a, b, evk_b, evk_a, qs, ps, dnum, rescale: bool):
+    """Relin(a x b) = (d0 + KS0(d2), d1 + KS1(d2)), NTT form; then optionally rescale_ntt."""
+    d = tensor_ntt(a, b, qs)
+    ks0, ks1 = keyswitch(d[2], evk_b, evk_a, qs, ps, dnum)
+    col = _mods_col(qs)
+    out = np.stack([(d[0] + ks0) % col, (d[1] + ks1) % col])
+    if rescale:
+        out = np.stack([rescale_ntt(out[0], qs), rescale_ntt(out[1], qs)])
+    return out
