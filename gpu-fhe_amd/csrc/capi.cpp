@@ -27,6 +27,8 @@ int check_window(const fhe_ctx* c, uint32_t limb0, uint32_t nlimbs, uint32_t lim
   return kOk;
 }
 
+}  // namespace
+
 // Internal workspace (grows on demand; allocation makes this path non-capturable).
 int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws) {
   if (*ws) return kOk;
@@ -41,8 +43,6 @@ int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws) {
   *ws = c->workspace;
   return kOk;
 }
-
-}  // namespace
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 

@@ -113,6 +113,9 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
                      const u64* evk_a, u32 batch, bool rescale, void* ws, hipStream_t s);
 size_t mul_relin_workspace_bytes(const fhe_ctx* c, u32 batch);
 
+// caller workspace, else the context's internal one grown to `bytes` (capi.cpp)
+int ensure_ws(const fhe_ctx* c, size_t bytes, void** ws);
+
 // ---- host (context.cpp) ----------------------------------------------------------------
 int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 K, u32 dnum,
                int device);

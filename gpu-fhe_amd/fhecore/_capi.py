@@ -60,6 +60,13 @@ SIGNATURES = {
     "fhe_graph_end": (_i32, [_vp, ctypes.POINTER(_vp)]),
     "fhe_graph_launch": (_i32, [_vp, _vp]),
     "fhe_graph_destroy": (_i32, [_vp]),
+    "fhe_sample": (_i32, [_vp, _vp, _u32, _u32, _u32, _i32, _u64, _u32, _vp]),
+    "fhe_keygen_secret": (_i32, [_vp, _vp, _u64, _vp]),
+    "fhe_keygen_public": (_i32, [_vp, _vp, _vp, _u64, _vp]),
+    "fhe_keygen_switch": (_i32, [_vp, _vp, _vp, _vp, _u64, _vp]),
+    "fhe_encrypt": (_i32, [_vp, _vp, _vp, _vp, _u64, _vp, _vp]),
+    "fhe_encrypt_sk": (_i32, [_vp, _vp, _vp, _vp, _u64, _vp]),
+    "fhe_decrypt": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _vp]),
     "fhe_prof_begin": (_i32, [_u32, _vp]),
     "fhe_prof_end": (_i32, [ctypes.POINTER(ctypes.c_float), _u32, ctypes.POINTER(_u32),
                             ctypes.c_char_p, _sz]),

@@ -285,6 +285,80 @@ class Context:
                                  _ptr(rot_a), batch, _ptr(ws), _stream(ct)), "fhe_rotate")
         return out
 
+    # ---- SURVEY.md §8(f) row 3: sampling, keys, encryption --------------------------------
+    KIND = {"uniform": 0, "ternary": 1, "error": 2}
+
+    def sample(self, kind: str, polys: int, seed: int, tag: int, limb0: int = 0, nlimbs=None):
+        """[polys, nlimbs, N] residues of a Philox4x32-10 draw (oracle: pyoracle.sample)."""
+        nl = (self.L + self.K - limb0) if nlimbs is None else nlimbs
+        out = torch.empty(polys, nl, self.n, dtype=torch.int64, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(load().fhe_sample(self._ptr, _ptr(out), polys, limb0, nl, self.KIND[kind],
+                                    seed, tag, _stream(out)), "fhe_sample")
+        return out
+
+    def keygen_secret(self, seed: int):
+        """Ternary secret, NTT form over all L + K limbs: [L + K, N]."""
+        sk = torch.empty(self.L + self.K, self.n, dtype=torch.int64, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(load().fhe_keygen_secret(self._ptr, _ptr(sk), seed, _stream(sk)), "fhe_keygen_secret")
+        return sk
+
+    def keygen_public(self, sk, seed: int):
+        pk = torch.empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(load().fhe_keygen_public(self._ptr, _ptr(pk), _ptr(sk), seed, _stream(pk)),
+                  "fhe_keygen_public")
+        return pk
+
+    def keygen_switch(self, sk, s_from, seed: int):
+        """Key-switch key from s_from ([L + K, N] NTT form) to sk: (evk_b, evk_a), each
+        [dnum, L + K, N] -- the operands of keyswitch / rotate / mul_relin."""
+        key = torch.empty(2, self.dnum, self.L + self.K, self.n, dtype=torch.int64, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(load().fhe_keygen_switch(self._ptr, _ptr(key), _ptr(sk), _ptr(s_from), seed,
+                                           _stream(key)), "fhe_keygen_switch")
+        return key[0], key[1]
+
+    def keygen_relin(self, sk, seed: int):
+        """Relinearisation key: switches s^2 to s."""
+        s2 = torch.empty_like(sk)
+        lib = load()
+        with torch.cuda.device(self.device):
+            check(lib.fhe_vec_mul(self._ptr, _ptr(s2), _ptr(sk), _ptr(sk), 1, 0, self.L + self.K,
+                                  _stream(sk)), "fhe_vec_mul")
+        return self.keygen_switch(sk, s2, seed)
+
+    def keygen_rotation(self, sk, galois_elt: int, seed: int):
+        """Rotation key for Galois element k: switches sigma_k(s) to s."""
+        return self.keygen_switch(sk, self.automorphism(sk, galois_elt, ntt_form=True), seed)
+
+    def encrypt(self, pt, pk, seed: int):
+        """Public-key encryption of an NTT-form plaintext [L, N] -> ciphertext [2, L, N]."""
+        ct = torch.empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(load().fhe_encrypt(self._ptr, _ptr(ct), _ptr(pt), _ptr(pk), seed, None,
+                                     _stream(ct)), "fhe_encrypt")
+        return ct
+
+    def encrypt_sk(self, pt, sk, seed: int):
+        ct = torch.empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(load().fhe_encrypt_sk(self._ptr, _ptr(ct), _ptr(pt), _ptr(sk), seed, _stream(ct)),
+                  "fhe_encrypt_sk")
+        return ct
+
+    def decrypt(self, ct, sk):
+        """ct [..., 2, l, N] (any level l <= L) -> plaintext c0 + c1 s [..., l, N], NTT form."""
+        _check_tensor(ct, "ct", (self.n,))
+        nl = ct.shape[-2]
+        batch = ct.numel() // (2 * nl * self.n)
+        pt = torch.empty(*ct.shape[:-3], nl, self.n, dtype=ct.dtype, device=ct.device)
+        with torch.cuda.device(self.device):
+            check(load().fhe_decrypt(self._ptr, _ptr(pt), _ptr(ct), _ptr(sk), batch, nl, _stream(ct)),
+                  "fhe_decrypt")
+        return pt
+
     # ---- SURVEY.md §8(f) row 4: fused multiply -> relinearise -> rescale ------------------
     def mul_relin(self, a, b, evk_b, evk_a, rescale: bool = True, workspace=None, out=None):
         """a, b [..., 2, L, N] NTT form -> Relin(a x b) [..., 2, L, N] (rescale: [..., 2, L-1, N]),

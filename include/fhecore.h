@@ -175,6 +175,30 @@ int fhe_deserialize(const fhe_ctx* ctx, const void* host_buf, size_t size, uint6
                     size_t dev_words, uint32_t* polys, uint32_t* limb0, uint32_t* nlimbs,
                     int* ntt_form, fhe_stream_t stream);
 
+/* ---- sampling, keys, encryption (not in the reference) ---------------
+ * Counter-based Philox4x32-10 randomness: every sample is a function of (seed, tag, poly, limb,
+ * coefficient), restated bit for bit by oracle/pyoracle.py.  kind: 0 uniform mod q, 1 ternary
+ * {-1, 0, 1}, 2 centred binomial eta = 21 (small kinds: one integer per coefficient on every limb).
+ * Keys are NTT form: sk [L + K][N] (all context limbs); pk [2][L][N] = (-a s + e, a);
+ * switch key [2][dnum][L + K][N] = (b part, a part) from s_from ([L + K][N], NTT form: s^2 for
+ * relinearisation, sigma_k(s) for rotation by Galois element k) to s -- the layout fhe_keyswitch,
+ * fhe_rotate and fhe_mul_relin take as (evk_b, evk_a).  Ciphertexts [2][L][N] NTT form;
+ * plaintexts [L][N] NTT form.  fhe_decrypt: pt = c0 + c1 s over the first nlimbs Q-limbs of
+ * `batch` ciphertexts [batch][2][nlimbs][N]. */
+int fhe_sample(const fhe_ctx* ctx, uint64_t* out, uint32_t polys, uint32_t limb0,
+               uint32_t nlimbs, int kind, uint64_t seed, uint32_t tag, fhe_stream_t stream);
+int fhe_keygen_secret(const fhe_ctx* ctx, uint64_t* sk, uint64_t seed, fhe_stream_t stream);
+int fhe_keygen_public(const fhe_ctx* ctx, uint64_t* pk, const uint64_t* sk, uint64_t seed,
+                      fhe_stream_t stream);
+int fhe_keygen_switch(const fhe_ctx* ctx, uint64_t* key, const uint64_t* sk,
+                      const uint64_t* s_from, uint64_t seed, fhe_stream_t stream);
+int fhe_encrypt(const fhe_ctx* ctx, uint64_t* ct, const uint64_t* pt, const uint64_t* pk,
+                uint64_t seed, void* workspace, fhe_stream_t stream);
+int fhe_encrypt_sk(const fhe_ctx* ctx, uint64_t* ct, const uint64_t* pt, const uint64_t* sk,
+                   uint64_t seed, fhe_stream_t stream);
+int fhe_decrypt(const fhe_ctx* ctx, uint64_t* pt, const uint64_t* ct, const uint64_t* sk,
+                uint32_t batch, uint32_t nlimbs, fhe_stream_t stream);
+
 /* ---- fused multiply -> relinearise -> rescale ------------------------
  * a, b [batch][2][L][N] NTT form; evk_b, evk_a [dnum][L + K][N] the relinearisation key (NTT
  * form, as for fhe_keyswitch).  out = Relin(a x b) [batch][2][L][N], or with rescale != 0 its

@@ -636,3 +636,110 @@ def mul_relin(a, b, evk_b, evk_a, qs, ps, dnum, rescale: bool):
     if rescale:
         out = np.stack([rescale_ntt(out[0], qs), rescale_ntt(out[1], qs)])
     return out
+
+
+# ---- sampling, keys, encryption (restating csrc/keygen.hip) -------------
+# Counter-based Philox4x32-10 (Salmon et al., "Parallel random numbers: as easy as 1, 2, 3",
+# SC'11 -- the Random123 construction), so each sample is a function of its coordinates.
+
+_M32 = 0xFFFFFFFF
+TAG = {"secret": 1, "pk_a": 2, "pk_e": 3, "ks_a": 0x100, "ks_e": 0x101, "enc_u": 32,
+       "enc_e0": 33, "enc_e1": 34, "enc_a": 35, "enc_e": 36}
+
+
+def philox4x32_10(c, k0, k1):
+    x, y, z, w = c
+    for _ in range(10):
+        p0, p1 = 0xD2511F53 * x, 0xCD9E8D57 * z
+        x, y, z, w = ((p1 >> 32) ^ y ^ k0) & _M32, p1 & _M32, ((p0 >> 32) ^ w ^ k1) & _M32, p0 & _M32
+        k0, k1 = (k0 + 0x9E3779B9) & _M32, (k1 + 0xBB67AE85) & _M32
+    return x, y, z, w
+
+
+def sample(kind: str, seed: int, tag: int, poly: int, limbs, n: int):
+    """(len(limbs), n) residues; limbs = [(ctx limb index, q)].  kind: uniform / ternary / error.
+    Small distributions draw one integer per coefficient, shared by every limb."""
+    k0, k1 = seed & _M32, (seed >> 32) & _M32
+    out = np.zeros((len(limbs), n), dtype=object)
+    if kind == "uniform":
+        for r, (li, q) in enumerate(limbs):
+            for c in range(n):
+                x, y, z, w = philox4x32_10((c, li, poly, tag), k0, k1)
+                lo, hi = (y << 32) | x, (w << 32) | z
+                out[r, c] = (hi * q + ((lo * q) >> 64)) >> 64
+        return out
+    vals = []
+    for c in range(n):
+        x, y, _, _ = philox4x32_10((c, _M32, poly, tag), k0, k1)
+        if kind == "ternary":
+            vals.append(x % 3 - 1)
+        else:
+            bits = (y << 32) | x
+            vals.append(bin(bits & 0x1FFFFF).count("1") - bin((bits >> 21) & 0x1FFFFF).count("1"))
+    for r, (_, q) in enumerate(limbs):
+        out[r] = [v % q for v in vals]
+    return out
+
+
+def keygen_secret(seed, allm, log_n):
+    n = 1 << log_n
+    s = sample("ternary", seed, TAG["secret"], 0, list(enumerate(allm)), n)
+    return rns_ntt_fwd(s, allm)
+
+
+def keygen_public(seed, sk_ntt, qs, log_n):
+    n = 1 << log_n
+    lim = list(enumerate(qs))
+    a = sample("uniform", seed, TAG["pk_a"], 0, lim, n)
+    e = rns_ntt_fwd(sample("error", seed, TAG["pk_e"], 0, lim, n), qs)
+    col = _mods_col(qs)
+    return np.stack([(e - a * np.asarray(sk_ntt)[:len(qs)]) % col, a])
+
+
+def keygen_switch(seed, sk_ntt, s_from_ntt, qs, ps, dnum, log_n):
+    """[2][dnum][L + K][N]: evk_j = (-a_j s + e_j + P g_j s_from, a_j) (same gadget as gen_relin_key)."""
+    n = 1 << log_n
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    allm = qs + ps
+    lim = list(enumerate(allm))
+    col = _mods_col(allm)
+    P = math.prod(ps)
+    kb, ka = [], []
+    for j, (lo, hi) in enumerate(digit_ranges(len(qs), dnum)):
+        a = sample("uniform", seed, TAG["ks_a"] + 2 * j, 0, lim, n)
+        e = rns_ntt_fwd(sample("error", seed, TAG["ks_e"] + 2 * j, 0, lim, n), allm)
+        b = (e - a * np.asarray(sk_ntt)) % col
+        for i in range(lo, hi):
+            b[i] = (b[i] + (P % qs[i]) * np.asarray(s_from_ntt)[i]) % qs[i]
+        kb.append(b)
+        ka.append(a)
+    return np.stack([np.stack(kb), np.stack(ka)])
+
+
+def encrypt(seed, pt_ntt, pk, qs, log_n):
+    n = 1 << log_n
+    lim = list(enumerate(qs))
+    col = _mods_col(qs)
+    u = rns_ntt_fwd(sample("ternary", seed, TAG["enc_u"], 0, lim, n), qs)
+    e0 = rns_ntt_fwd(sample("error", seed, TAG["enc_e0"], 0, lim, n), qs)
+    e1 = rns_ntt_fwd(sample("error", seed, TAG["enc_e1"], 0, lim, n), qs)
+    pk = np.asarray(pk, dtype=object)
+    return np.stack([(e0 + pk[0] * u + np.asarray(pt_ntt, dtype=object)) % col,
+                     (e1 + pk[1] * u) % col])
+
+
+def encrypt_sk(seed, pt_ntt, sk_ntt, qs, log_n):
+    n = 1 << log_n
+    lim = list(enumerate(qs))
+    col = _mods_col(qs)
+    a = sample("uniform", seed, TAG["enc_a"], 0, lim, n)
+    e = rns_ntt_fwd(sample("error", seed, TAG["enc_e"], 0, lim, n), qs)
+    return np.stack([(e - a * np.asarray(sk_ntt)[:len(qs)] + np.asarray(pt_ntt, dtype=object)) % col,
+                     a])
+
+
+def decrypt(ct, sk_ntt, qs):
+    col = _mods_col(qs)
+    ct = np.asarray(ct, dtype=object)
+    return (ct[0] + ct[1] * np.asarray(sk_ntt, dtype=object)[:len(qs)]) % col

@@ -210,3 +210,27 @@ def test_rotation_decrypts_to_rotated_message():
                                        [qs[0]])[0]
     want = [int(v) - qs[0] if int(v) > qs[0] // 2 else int(v) for v in want]
     assert max(abs(int(d) - w) for d, w in zip(dec, want)) < 1 << 20
+
+
+# ---- Philox and samplers ---------------------------------------------
+
+def test_philox_known_answers():
+    """Random123's published known-answer vectors for philox4x32-10 (kat_vectors)."""
+    f = pyoracle.philox4x32_10
+    assert f((0, 0, 0, 0), 0, 0) == (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)
+    assert f((0xffffffff,) * 4, 0xffffffff, 0xffffffff) == (0x408f276d, 0x41c83b0e, 0xa20bc7c6,
+                                                            0x6d5451fd)
+    assert f((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), 0xa4093822, 0x299f31d0) == (
+        0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)
+
+
+def test_sampler_distributions():
+    n, q = 4096, pyoracle.gen_moduli(12, 1)[0]
+    t = [int(v) for v in pyoracle.sample("ternary", 7, 1, 0, [(0, q)], n)[0]]
+    t = [v - q if v > q // 2 else v for v in t]
+    assert set(t) == {-1, 0, 1} and all(abs(t.count(v) / n - 1 / 3) < 0.03 for v in (-1, 0, 1))
+    e = [int(v) for v in pyoracle.sample("error", 7, 3, 0, [(0, q)], n)[0]]
+    e = [v - q if v > q // 2 else v for v in e]
+    assert max(abs(v) for v in e) <= 21 and abs(np.mean(e)) < 0.2 and abs(np.var(e) - 10.5) < 1.0
+    u = [int(v) for v in pyoracle.sample("uniform", 7, 2, 0, [(0, q)], n)[0]]
+    assert all(0 <= v < q for v in u) and abs(np.mean(u) / q - 0.5) < 0.02
