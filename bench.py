@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch"], default="hommult")
+    ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch", "mulrelin"],
+                    default="hommult")
     ap.add_argument("--batch", type=int, default=16, help="ciphertexts per GPU per step")
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
@@ -281,10 +282,49 @@ def run_keyswitch(args, world, rank):
     return out, None
 
 
+def run_mulrelin(args, world, rank):
+    """ct x ct multiply -> relinearise -> rescale, NTT form, at the key-switch
+    configuration (N = 2^16, L = 16, K = 4, dnum = 4), captured once in a HIP graph and replayed.
+    Single-device per rank (replicas: no collective; the sharded key-switch is --workload
+    keyswitch)."""
+    L, K, dnum = 16, 4, 4
+    n = 1 << args.log_n
+    ctx = fc.Context(args.log_n, L=L, K=K, dnum=dnum)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(11 + rank)
+    B = args.batch
+    a = uniform_limbs(gen, ctx.moduli, (B, 2), n)
+    b = uniform_limbs(gen, ctx.moduli, (B, 2), n)
+    kb = uniform_limbs(gen, ctx.all_moduli, (dnum,), n)
+    ka = uniform_limbs(gen, ctx.all_moduli, (dnum,), n)
+    ws = ctx.workspace(load().fhe_mul_relin_workspace(ctx.handle, B))
+    out = torch.empty(B, 2, L - 1, n, dtype=torch.int64, device="cuda")
+    side = torch.cuda.Stream()  # the legacy default stream cannot be captured
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        ctx.mul_relin(a, b, kb, ka, rescale=True, workspace=ws, out=out)  # eager once
+        with fc.Graph() as g:
+            ctx.mul_relin(a, b, kb, ka, rescale=True, workspace=ws, out=out)
+        dt, kavg = timed(g.launch, args, world, 4)
+    per_s = B * args.steps * world / dt
+    # per multiply: read 2 cts (4 L limbs), the key once per batch, write 2 (L-1) limbs
+    alg = (B * (4 * L + 2 * (L - 1)) + dnum * 2 * (L + K)) * n * 8 // B
+    out_line = {"metric": "mult+relin+rescale/sec at N=2^16, L=16, K=4, dnum=4 (NTT form, HIP graph)",
+                "value": round(per_s, 2), "unit": "mul_relin/s",
+                "ms_per_step": round(dt / args.steps * 1e3, 4),
+                "config": {"workload": "ct x ct multiply + relinearise + rescale (SURVEY §8f row 4)",
+                           "log_n": args.log_n, "L": L, "K": K, "dnum": dnum, "batch": B,
+                           "parallelism": f"replicas x{world}"},
+                "roofline": roofline("mul_relin (whole pipeline)", alg, dt / (B * args.steps) * 1e3 * world,
+                                     {"log_n": args.log_n, "L": L})}
+    return out_line, None
+
+
 def main():
     args = parse()
     world, rank = dist_setup(args)
-    run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch}[args.workload]
+    run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch,
+           "mulrelin": run_mulrelin}[args.workload]
     out, cpu = run(args, world, rank)
     if rank == 0:
         line = {"metric": out.pop("metric"), "value": out.pop("value"), "unit": out.pop("unit"),
