@@ -43,8 +43,10 @@ METRIC = "NTTs/sec + HomMult/sec at N=2^16, 8 RNS limbs; achieved HBM GB/s vs pe
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # the chip ramps its clock up over the first ~50 ms of sustained load: short warmups measure the
+    # ramp (W=5, K=20 reads ~15 % low at N=2^16, L=8); the defaults time the sustained rate
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch", "mulrelin"],
                     default="hommult")
     ap.add_argument("--batch", type=int, default=16, help="ciphertexts per GPU per step")
@@ -104,8 +106,9 @@ def timed(fn, args, world, max_marks):
     dt = time.perf_counter() - t0
     ms = (ctypes.c_float * max_marks)()
     cnt = ctypes.c_uint32()
-    names = ctypes.create_string_buffer(1 << 16)
-    check(lib.fhe_prof_end(ms, max_marks, ctypes.byref(cnt), names, 1 << 16), "fhe_prof_end")
+    names = ctypes.create_string_buffer(32 * max_marks + 64)
+    check(lib.fhe_prof_end(ms, max_marks, ctypes.byref(cnt), names, 32 * max_marks + 64),
+          "fhe_prof_end")
     per = {}
     for nm, v in zip(names.value.decode().split("\n"), ms[: cnt.value]):
         per.setdefault(nm, []).append(v)

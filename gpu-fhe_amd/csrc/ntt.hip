@@ -480,7 +480,7 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     const ulonglong2* twk = tw;
     if constexpr (LOOPED || GATHER) asm volatile("" : "+s"(twk));
     if constexpr (k == 0)
-      round_compute<LOGR, KB, LO, FWD, F, GATHER>(x, tp, twk, base, q, nf0, nf1, hook);
+      round_compute<LOGR, KB, LO, FWD, F, GATHER || LOOPED>(x, tp, twk, base, q, nf0, nf1, hook);
     else
       round_compute<LOGR, KB, LO, FWD, F, GATHER>(x, tp, twk, base, q, nf0, nf1);
 #endif
@@ -563,7 +563,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(cur.s), sub}, t, x);
   while (true) {
     const u32 nx = it + gridDim.x;
-    const bool more = kLoopCol && nx < items;
+    const bool more = kLoopCol && FWD && nx < items;
     const Item nxt = more ? decode(nx) : cur;
     auto prefetch = [&] {
       if (more) pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(nxt.s), sub}, t, y);
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       nf0 = nfold[4 * cur.limb];
       nf1 = nfold[4 * cur.limb + 1];
     }
-    pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol>(
+    pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol && FWD>(
         x, GView<G::R2>{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
         nf0, nf1, prefetch);
     if (!more) break;
@@ -828,7 +828,7 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
     k_ntt_row<LOGN, false><<<item_grid<k_ntt_row<LOGN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
         src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv, c->d_mods);
     prof_mark(s, "ntt_row_inv");
-    k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
+    k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, false>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
         dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv, c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_inv");
   }
@@ -857,7 +857,7 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   prof_mark(s, "hm_row_tensor");
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
-  k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, kLoopCol>(c, G::THR_C, ii), G::THR_C, 0, s>>>(
+  k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, false>(c, G::THR_C, ii), G::THR_C, 0, s>>>(
       d, nullptr, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv, c->d_nfold + 2,
       c->d_mods);
   prof_mark(s, "hm_col_inv");
