@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "modarith.hpp"
@@ -57,6 +58,10 @@ struct fhe_ctx {
 
   void* workspace = nullptr;
   size_t workspace_bytes = 0;
+  // helper stream for split-batch HomMult (created on first use; fork/join by events)
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t aux_fork = nullptr, aux_join = nullptr;
+  std::mutex aux_mutex;
 };
 
 namespace fhe {
