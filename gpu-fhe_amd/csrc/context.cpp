@@ -208,6 +208,8 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
   auto* c = new fhe_ctx();
   c->device = device;
   c->num_cus = cus;
+  c->lz16 = true;
+  for (u64 m : mods) c->lz16 = c->lz16 && m < (1ull << 60);
   c->log_n = log_n;
   c->n = n;
   c->L = L;

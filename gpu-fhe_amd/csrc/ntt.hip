@@ -240,6 +240,17 @@ struct NoHook {
   __device__ __forceinline__ void operator()() const {}
 };
 
+// Forward lazy ranges (FHE_BFLY = 2), in units of q.  A CT stage maps X-operands below r q to
+// outputs below (r' + 3) q, where r' = r unless r + 3 would exceed the headroom H (values must stay
+// below H q <= 2^64), in which case X is first reduced by H/2 q (r' = H/2).  H = 16 needs q < 2^60
+// and subtracts at about every other stage; H = 8 (q < 2^61) at every stage once warm.
+constexpr int fwd_stage_out(int r, int H) { return (r + 3 > H ? H / 2 : r) + 3; }
+constexpr int fwd_range(int r0, int stages, int H) {
+  int r = r0;
+  for (int i = 0; i < stages; ++i) r = fwd_stage_out(r, H);
+  return r;
+}
+
 // Runs one round's butterfly stages on the 16 values a thread holds in registers.
 // Element j sits at sub-transform position tp | Lay::jpos(j).  `base` selects the twiddle rows:
 // local stage st, group g reads tw[(base << st) + g] (base = 1 for the column pass, R1 + row for
@@ -249,7 +260,8 @@ struct NoHook {
 // GATHER = false leaves the twiddle loads to the scheduler, next to their butterflies (better for
 // the column pass, whose twiddles are few and shared); true issues them all first (the row passes:
 // per-lane twiddles from L2, whose latency then overlaps instead of stalling each stage).
-template <int LOGR, int KB, int LO, bool FWD, int FIN, bool GATHER = false, class Hook = NoHook>
+template <int LOGR, int KB, int LO, bool FWD, int FIN, bool GATHER = false, int H = 8,
+          int RIN = 8, class Hook = NoHook>
 __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
                                               const ulonglong2* __restrict__ tw, const u32 base,
                                               const u64 q, const ulonglong2 nf0,
@@ -284,6 +296,41 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
   [[maybe_unused]] const u64 q4 = 4 * q;
   asm("" : "+s"(q3));
   if constexpr (FWD) {
+#if FHE_BFLY == 2
+    // CT: X-operands below r q (the static range of this stage, fwd_range), reduced by H/2 q
+    // only when the stage would outgrow H q; v = w x[jj] in [0, 3q); outputs below (r' + 3) q
+    [[maybe_unused]] const u64 qh = (u64)(H / 2) * q;
+    static_for<0, KB>([&](auto sc) {
+      constexpr int done = decltype(sc)::value;
+      constexpr int b = KB - 1 - done;
+      constexpr int rin = fwd_range(RIN, done, H);
+      constexpr bool reduce = rin + 3 > H;
+      const int bitpos = LO + b;
+      const int st = LOGR - 1 - bitpos;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        if (j & (1 << b)) continue;
+        const int jj = j | (1 << b);
+        const ulonglong2 w = twiddle(b, j, bitpos, st);
+        const u64 u = reduce ? csub(x[j], qh) : x[j];
+        const u64 v = shoup_q3(x[jj], w.x, w.y, nq);
+        x[j] = u + v;
+        x[jj] = u - v + q3;
+      }
+    });
+    if constexpr (FIN == kFinalFwd || FIN == kFinalFwd2) {
+      // from below r_out q down to [0, q) (kFinalFwd) or [0, 2q) (kFinalFwd2) by halving steps
+      constexpr int rout = fwd_range(RIN, KB, H);
+      constexpr int stop = FIN == kFinalFwd ? 1 : 2;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        static_for<0, 5>([&](auto ci) {
+          constexpr int c = 16 >> decltype(ci)::value;  // 16, 8, 4, 2, 1
+          if constexpr (c >= stop && c < rout) x[j] = csub(x[j], (u64)c * q);
+        });
+      }
+    }
+#else
 #pragma unroll
     for (int b = KB - 1; b >= 0; --b) {
       const int bitpos = LO + b;
@@ -293,13 +340,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
         const ulonglong2 w = twiddle(b, j, bitpos, st);
-#if FHE_BFLY == 2
-        // CT: x in [0, 8q): u = x mod 4q in [0, 4q); v = w x[jj] in [0, 3q); outputs in [0, 7q)
-        const u64 u = csub(x[j], q4);
-        const u64 v = shoup_q3(x[jj], w.x, w.y, nq);
-        x[j] = u + v;
-        x[jj] = u - v + q3;
-#elif FHE_BFLY == 1
+#if FHE_BFLY == 1
         const u64 u = csub_fast(x[j], nq2);
         const u64 v = shoup_fast(x[jj], w.x, w.y, nq);
         x[j] = u + v;
@@ -316,14 +357,11 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
     if constexpr (FIN == kFinalFwd || FIN == kFinalFwd2) {
 #pragma unroll
       for (int j = 0; j < E; ++j) {
-#if FHE_BFLY == 2
-        x[j] = csub(csub(x[j], q4), q2);
-#else
         x[j] = csub(x[j], q2);
-#endif
         if constexpr (FIN == kFinalFwd) x[j] = csub(x[j], q);
       }
     }
+#endif
   } else {
 #pragma unroll
     for (int b = 0; b < KB; ++b) {
@@ -453,8 +491,9 @@ __device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
 // call it (it contains the exchange fences; the first one also orders this item's LDS writes
 // after the previous item's LDS reads).
 // `hook` runs once round 0's twiddle loads are in flight (the item loops' prefetch).
-template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, bool LOOPED, class GOut, class LV,
-          class Hook = NoHook>
+// H / R0: forward headroom and input range of the pass (fwd_range), in units of q.
+template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, bool LOOPED, int H, int R0,
+          class GOut, class LV, class Hook = NoHook>
 __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const LV& lv, u32 t,
                                          const ulonglong2* __restrict__ tw, u32 base, u64 q,
                                          ulonglong2 nf0, ulonglong2 nf1,
@@ -465,6 +504,7 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     constexpr int KB = FWD ? Rd::kb(k) : Rd::kb_inv(k);
     constexpr int LO = FWD ? Rd::lo_fwd(k) : Rd::lo_inv(k);
     constexpr int F = (k == Rd::NR - 1) ? FIN : kNotFinal;
+    constexpr int RIN = fwd_range(R0, Rd::lo_fwd(0) + Rd::kb(0) - (LO + KB), H);  // stages before
     using Lay = Layout<LOGR, KB, LO>;
     const u32 tp = Lay::tpos(t);
     if constexpr (k > 0) {
@@ -480,9 +520,10 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     const ulonglong2* twk = tw;
     if constexpr (LOOPED || GATHER) asm volatile("" : "+s"(twk));
     if constexpr (k == 0)
-      round_compute<LOGR, KB, LO, FWD, F, GATHER || LOOPED>(x, tp, twk, base, q, nf0, nf1, hook);
+      round_compute<LOGR, KB, LO, FWD, F, GATHER || LOOPED, H, RIN>(x, tp, twk, base, q, nf0, nf1,
+                                                                   hook);
     else
-      round_compute<LOGR, KB, LO, FWD, F, GATHER>(x, tp, twk, base, q, nf0, nf1);
+      round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN>(x, tp, twk, base, q, nf0, nf1);
 #endif
     if constexpr (k == Rd::NR - 1) {
 #if FHE_NTT_ABLATE == 2
@@ -530,7 +571,7 @@ struct Geo {
 // multiple of 8, so an item keeps the XCD (blockIdx % 8) its index maps to.
 
 // Column pass over items (p, l, tile) of src/dst [polys][nlimbs][N] via PolyMap.
-template <int LOGN, bool FWD>
+template <int LOGN, bool FWD, int H = 8>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_ntt_col(const u64* __restrict__ src,
                                                       const u64* __restrict__ src2,
@@ -573,7 +614,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       nf0 = nfold[4 * cur.limb];
       nf1 = nfold[4 * cur.limb + 1];
     }
-    pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol && FWD>(
+    pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
         x, GView<G::R2>{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
         nf0, nf1, prefetch);
     if (!more) break;
@@ -586,7 +627,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
 
 // Row pass over items (l, p, tile): the limb follows the XCD and the poly varies fastest, so the
 // workgroups of one XCD reuse a row's twiddles while they are hot.
-template <int LOGN, bool FWD>
+template <int LOGN, bool FWD, int H = 8>
 __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
                                                       u64* __restrict__ dst, u32 nlimbs,
                                                       u32 limb0, PolyMap pm, u32 items,
@@ -624,7 +665,8 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
     auto prefetch = [&] {
       if (more) pass_load<G::N2, FWD>(GView<1>{const_cast<u64*>(src) + nxt.src, lane}, t, y);
     };
-    pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, kLoopRow>(
+    pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, kLoopRow, H,
+             fwd_range(1, G::N1, H)>(
         x, GView<1>{dst + cur.dst, lane}, lv, t, tw_all + (u64)cur.limb * N,
 #if FHE_NTT_ABLATE == 3  // timing-only build: every row uses row 0's twiddles (cache-resident)
         (u32)G::R1,
@@ -665,7 +707,7 @@ struct HmGeo {
   static constexpr int SYNC_ROUND = (POLY_MAJOR || LANES_ROW <= 64) ? kWaveSync : kBlockSync;
 };
 
-template <int LOGN>
+template <int LOGN, int HR = 8>
 __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
                                                           u64* __restrict__ d, u32 nlimbs,
                                                           u32 limb0,
@@ -714,6 +756,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
     constexpr int KB = Rd::kb(k);
     constexpr int LO = Rd::lo_fwd(k);
     constexpr int F = (k == Rd::NR - 1) ? kFinalFwd2 : kNotFinal;
+    constexpr int RIN = fwd_range(fwd_range(1, G::N1, HR), G::N2 - (LO + KB), HR);
     using Lay = Layout<G::N2, KB, LO>;
     const u32 tp = Lay::tpos(t);
     if constexpr (k == 0) {
@@ -723,7 +766,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
       lds_sync<SY>();
       own.template load<Lay>(v, tp);
     }
-    round_compute<G::N2, KB, LO, true, F, true>(v, tp, tf, base, q, {0, 0}, {0, 0});
+    round_compute<G::N2, KB, LO, true, F, true, HR, RIN>(v, tp, tf, base, q, {0, 0}, {0, 0});
     if constexpr (k < Rd::NR - 1) {
       if (k > 0) lds_sync<SY>();
       own.template store<Lay>(v, tp);
@@ -808,7 +851,7 @@ dim3 item_grid(const fhe_ctx* c, int threads, u64 items) {
   return dim3((u32)g);
 }
 
-template <int LOGN>
+template <int LOGN, int HD>
 int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* dst,
                  u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
   using G = Geo<LOGN>;
@@ -818,10 +861,10 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   const PolyMap pd = flat_map(dpstride);
   const u64 ic = pl * G::TILES_C, ir = pl * G::TILES_R;
   if (fwd) {
-    k_ntt_col<LOGN, true><<<item_grid<k_ntt_col<LOGN, true>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
+    k_ntt_col<LOGN, true, HD><<<item_grid<k_ntt_col<LOGN, true, HD>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
         src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd, c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_fwd");
-    k_ntt_row<LOGN, true><<<item_grid<k_ntt_row<LOGN, true>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
+    k_ntt_row<LOGN, true, HD><<<item_grid<k_ntt_row<LOGN, true, HD>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
         dst, dst, nlimbs, limb0, pd, (u32)ir, c->d_tw_fwd, c->d_mods);
     prof_mark(s, "ntt_row_fwd");
   } else {
@@ -836,7 +879,7 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   return kOk;
 }
 
-template <int LOGN>
+template <int LOGN, int HD>
 int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                      u32 nlimbs, u64* x, hipStream_t s) {
   using G = Geo<LOGN>;
@@ -847,12 +890,12 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   // over the 4 polys of every ciphertext pair (group of 4: slots 0, 1 from a, slots 2, 3 from b)
   const PolyMap to_x{4, 2 * limbN, limbN, 4 * limbN, limbN, 2};
   const u64 ic = (u64)batch * 4 * nlimbs * G::TILES_C;
-  k_ntt_col<LOGN, true><<<item_grid<k_ntt_col<LOGN, true>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0,
+  k_ntt_col<LOGN, true, HD><<<item_grid<k_ntt_col<LOGN, true, HD>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0,
                           s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic, c->d_tw_fwd, c->d_nfold,
                                c->d_mods);
   prof_mark(s, "hm_col_fwd");
   const dim3 gh((u32)((u64)batch * nlimbs * H::TILES));
-  k_hommult_row<LOGN><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd, c->d_tw_inv,
+  k_hommult_row<LOGN, HD><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd, c->d_tw_inv,
                                             c->d_mods);
   prof_mark(s, "hm_row_tensor");
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
@@ -880,7 +923,10 @@ int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstr
   switch (c->log_n) {
 #define X(n) \
   case n:    \
-    return ntt_dispatch<n>(c, forward, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
+    return c->lz16 ? ntt_dispatch<n, 16>(c, forward, src, spstride, dst, dpstride, polys, limb0, \
+                                         nlimbs, s)                                            \
+                   : ntt_dispatch<n, 8>(c, forward, src, spstride, dst, dpstride, polys, limb0,  \
+                                        nlimbs, s);
     FHE_LOGN_CASES(X)
 #undef X
   }
@@ -897,7 +943,8 @@ static int hommult_chunk(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u
   switch (c->log_n) {
 #define X(n) \
   case n:    \
-    return hommult_dispatch<n>(c, d, a, b, batch, limb0, nlimbs, x, s);
+    return c->lz16 ? hommult_dispatch<n, 16>(c, d, a, b, batch, limb0, nlimbs, x, s) \
+                   : hommult_dispatch<n, 8>(c, d, a, b, batch, limb0, nlimbs, x, s);
     FHE_LOGN_CASES(X)
 #undef X
   }

@@ -294,3 +294,22 @@ def test_dist_sharded_keyswitch_single_rank_on_gpu(fc):
                                LimbShard(L, 1, 0))
     r0, r1 = coracle.keyswitch(d2, eb, ea, ctx.moduli, ctx.special, dnum)
     assert (fc.to_host(k0) == r0).all() and (fc.to_host(k1) == r1).all()
+
+
+@pytest.mark.parametrize("bits", [60, 61])
+def test_lazy_headroom_variants_match_oracle(fc, bits):
+    """Contexts whose moduli are all below 2^60 run the forward NTTs lazy up to 16q; 61-bit primes
+    take the 8q variant (ntt.hip fwd_range).  Both must be bit-exact (NTT and HomMult)."""
+    log_n = 12
+    mods = fc.gen_moduli(log_n, 3, bits=bits)
+    assert (max(mods) >= 1 << 60) == (bits == 61)
+    ctx = fc.Context(log_n, moduli=mods)
+    x = rand(mods, log_n, (2,), seed=bits)
+    t = fc.to_device(x)
+    ctx.ntt_(t)
+    assert (fc.to_host(t) == coracle.ntt_fwd(x, mods)).all()
+    a = rand(mods, log_n, (2, 2), seed=bits + 1)
+    b = rand(mods, log_n, (2, 2), seed=bits + 2)
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    for i in range(2):
+        assert (d[i] == coracle.hommult(a[i], b[i], mods)).all()
