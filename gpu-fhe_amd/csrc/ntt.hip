@@ -472,6 +472,31 @@ struct LView {
   }
 };
 
+// LDS view of the column pass: position p of column `sub` (base s = lds + sub) in a tile of S
+// columns, no padding.  S >= 32: rows of S words, and a half-wavefront (32 lanes = 32 columns)
+// touches 32 distinct banks.  S = 16 (N1 = 8): rows pair into 32-word blocks, and the half each
+// row takes is swapped by bit 4 of p, so both exchange patterns (p = t + 16 j and p = 16 t + j,
+// t and t + 1 in one half-wavefront) land in different halves.  32 KB per workgroup instead of
+// 34 KB with a pad column: 5 workgroups per CU instead of 4.
+template <int S>
+struct LViewC {
+  u64* s;
+  __device__ __forceinline__ u32 idx(u32 p) const {
+    if constexpr (S >= 32) return p * S;
+    return (p >> 1) * 32 + (((p ^ (p >> 4)) & 1u) << 4);
+  }
+  template <class Lay>
+  __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
+#pragma unroll
+    for (int j = 0; j < kE; ++j) x[j] = s[idx(tp | Lay::jpos(j))];
+  }
+  template <class Lay>
+  __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
+#pragma unroll
+    for (int j = 0; j < kE; ++j) s[idx(tp | Lay::jpos(j))] = x[j];
+  }
+};
+
 // Round-0 global load of one sub-transform into registers (issued ahead of the work that needs
 // it: the kernels below prefetch their next item while computing the current one).
 template <int LOGR, bool FWD, class GIn>
@@ -551,8 +576,8 @@ struct Geo {
   static constexpr int TPS_C = R1 >> kElog;
   static constexpr int SUBS_C = (kColThreads / TPS_C) < R2 ? (kColThreads / TPS_C) : R2;
   static constexpr int THR_C = SUBS_C * TPS_C;
-  static constexpr int CS = SUBS_C + 1;  // LDS row stride (words)
-  static constexpr int LDS_C = R1 * CS;
+  static constexpr int LDS_C = R1 * SUBS_C;  // LViewC: no padding
+  static_assert(SUBS_C == 16 || SUBS_C >= 32, "column LDS layout assumes 16 or >= 32 columns");
   static constexpr int TILES_C = R2 / SUBS_C;
   // row pass: SUBS_R rows per workgroup, lanes run along a row
   static constexpr int TPS_R = R2 >> kElog;
@@ -584,7 +609,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[G::LDS_C];
   const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
-  const LView<G::CS, false> lv{lds + sub};
+  const LViewC<G::SUBS_C> lv{lds + sub};
   struct Item {  // all wave-uniform
     u32 limb;
     const u64* s;
