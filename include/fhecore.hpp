@@ -74,7 +74,7 @@ class Context {
  public:
   Context(uint32_t log_n, const std::vector<uint64_t>& q, const std::vector<uint64_t>& p = {},
           uint32_t dnum = 1, int device = 0)
-      : log_n_(log_n), L_((uint32_t)q.size()), K_((uint32_t)p.size()) {
+      : log_n_(log_n), L_((uint32_t)q.size()), K_((uint32_t)p.size()), dnum_(p.empty() ? 0 : dnum) {
     check(fhe_ctx_create(&c_, log_n, q.data(), L_, p.empty() ? nullptr : p.data(), K_,
                          K_ ? dnum : 0, device),
           "fhe_ctx_create");
@@ -91,7 +91,7 @@ class Context {
     if (c_) fhe_ctx_destroy(c_);
   }
   Context(Context&& o) noexcept
-      : c_(std::exchange(o.c_, nullptr)), log_n_(o.log_n_), L_(o.L_), K_(o.K_) {}
+      : c_(std::exchange(o.c_, nullptr)), log_n_(o.log_n_), L_(o.L_), K_(o.K_), dnum_(o.dnum_) {}
   Context(const Context&) = delete;
   Context& operator=(const Context&) = delete;
 
@@ -100,10 +100,70 @@ class Context {
   uint64_t n() const { return 1ull << log_n_; }
   uint32_t L() const { return L_; }
   uint32_t K() const { return K_; }
+  uint32_t dnum() const { return dnum_; }
 
  private:
   fhe_ctx* c_ = nullptr;
-  uint32_t log_n_, L_, K_;
+  uint32_t log_n_, L_, K_, dnum_;
+};
+
+// Keys, NTT form: secret [L+K][N], public [2][L][N], switch
+// [2][dnum][L+K][N] = (b part, a part) -- the (evk_b, evk_a) of keyswitch / rotate / mul_relin.
+struct SecretKey {
+  DeviceBuffer s;
+};
+struct PublicKey {
+  DeviceBuffer pk;
+};
+struct SwitchKey {
+  DeviceBuffer key;
+  size_t half = 0;  // words of the b part
+  const uint64_t* b() const { return key.data(); }
+  const uint64_t* a() const { return key.data() + half; }
+};
+
+// Counter-based (Philox4x32-10) key generation: every key is a function of (context, seeds).
+class KeyGenerator {
+ public:
+  KeyGenerator(const Context& ctx, uint64_t seed, hipStream_t stream = nullptr)
+      : ctx_(ctx), s_(stream) {
+    sk_.s = DeviceBuffer((size_t)(ctx.L() + ctx.K()) * ctx.n());
+    check(fhe_keygen_secret(ctx.get(), sk_.s.data(), seed, s_), "fhe_keygen_secret");
+  }
+  const SecretKey& secret() const { return sk_; }
+  PublicKey public_key(uint64_t seed) const {
+    PublicKey p{DeviceBuffer((size_t)2 * ctx_.L() * ctx_.n())};
+    check(fhe_keygen_public(ctx_.get(), p.pk.data(), sk_.s.data(), seed, s_), "fhe_keygen_public");
+    return p;
+  }
+  // switches s^2 to s
+  SwitchKey relin_key(uint64_t seed) const {
+    DeviceBuffer s2((size_t)(ctx_.L() + ctx_.K()) * ctx_.n());
+    check(fhe_vec_mul(ctx_.get(), s2.data(), sk_.s.data(), sk_.s.data(), 1, 0, ctx_.L() + ctx_.K(), s_),
+          "fhe_vec_mul");
+    return switch_key(s2, seed);
+  }
+  // switches sigma_k(s) to s
+  SwitchKey rotation_key(uint32_t galois_elt, uint64_t seed) const {
+    DeviceBuffer sk((size_t)(ctx_.L() + ctx_.K()) * ctx_.n());
+    check(fhe_automorphism(ctx_.get(), sk.data(), sk_.s.data(), 1, 0, ctx_.L() + ctx_.K(), galois_elt,
+                           1, s_),
+          "fhe_automorphism");
+    return switch_key(sk, seed);
+  }
+
+ private:
+  SwitchKey switch_key(const DeviceBuffer& s_from, uint64_t seed) const {
+    SwitchKey k;
+    k.half = (size_t)ctx_.dnum() * (ctx_.L() + ctx_.K()) * ctx_.n();
+    k.key = DeviceBuffer(2 * k.half);
+    check(fhe_keygen_switch(ctx_.get(), k.key.data(), sk_.s.data(), s_from.data(), seed, s_),
+          "fhe_keygen_switch");
+    return k;
+  }
+  const Context& ctx_;
+  hipStream_t s_;
+  SecretKey sk_;
 };
 
 // A ciphertext (or plain polynomial when components == 1): [components][limbs][N] residues.
@@ -169,6 +229,34 @@ class Evaluator {
           "fhe_keyswitch");
     return {std::move(k0), std::move(k1)};
   }
+  // Public-key encryption of an NTT-form plaintext (1 component, L limbs) -> [2][L][N] NTT form.
+  Ciphertext encrypt(const Ciphertext& pt, const PublicKey& pk, uint64_t seed) const {
+    if (pt.components != 1 || pt.limbs != ctx_.L() || !pt.ntt_form)
+      throw Error(FHE_EINVAL, "encrypt: need a 1-component NTT-form plaintext over L limbs");
+    Ciphertext ct(ctx_, 2, ctx_.L(), true);
+    check(fhe_encrypt(ctx_.get(), ct.data(), pt.data(), pk.pk.data(), seed, nullptr, s_), "fhe_encrypt");
+    return ct;
+  }
+  // c0 + c1 s over the ciphertext's limbs -> 1-component NTT-form plaintext.
+  Ciphertext decrypt(const Ciphertext& ct, const SecretKey& sk) const {
+    if (ct.components != 2 || !ct.ntt_form) throw Error(FHE_EINVAL, "decrypt: need an NTT-form ciphertext");
+    Ciphertext pt(ctx_, 1, ct.limbs, true);
+    check(fhe_decrypt(ctx_.get(), pt.data(), ct.data(), sk.s.data(), 1, ct.limbs, s_), "fhe_decrypt");
+    return pt;
+  }
+  // Relin(a x b), optionally rescaled; NTT form over L limbs in.
+  Ciphertext mul_relin(const Ciphertext& a, const Ciphertext& b, const SwitchKey& rk, bool rescale) const {
+    same(a, b, "mul_relin");
+    if (a.components != 2 || !a.ntt_form || a.limbs != ctx_.L())
+      throw Error(FHE_EINVAL, "mul_relin: need 2-component NTT-form ciphertexts over L limbs");
+    Ciphertext out(ctx_, 2, ctx_.L() - (rescale ? 1 : 0), true);
+    const size_t need = fhe_mul_relin_workspace(ctx_.get(), 1);
+    if (ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
+    check(fhe_mul_relin(ctx_.get(), out.data(), a.data(), b.data(), rk.b(), rk.a(), 1, rescale ? 1 : 0,
+                        ws_.data(), s_),
+          "fhe_mul_relin");
+    return out;
+  }
   // Divide-and-round by the last modulus: drops one limb, keeps the form.
   Ciphertext rescale(const Ciphertext& x) const {
     if (x.limbs < 2) throw Error(FHE_EINVAL, "rescale: need at least 2 limbs");
@@ -200,6 +288,16 @@ class Evaluator {
     if (ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
     check(fhe_rotate(ctx_.get(), out.data(), ct.data(), galois_elt, rot_b.data(), rot_a.data(), 1,
                      ws_.data(), s_),
+          "fhe_rotate");
+    return out;
+  }
+  Ciphertext rotate(const Ciphertext& ct, uint32_t galois_elt, const SwitchKey& key) const {
+    if (ct.components != 2 || !ct.ntt_form || ct.limbs != ctx_.L())
+      throw Error(FHE_EINVAL, "rotate: need a 2-component NTT-form ciphertext over L limbs");
+    Ciphertext out(ctx_, 2, ct.limbs, true);
+    const size_t need = fhe_rotate_workspace(ctx_.get(), 1);
+    if (ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
+    check(fhe_rotate(ctx_.get(), out.data(), ct.data(), galois_elt, key.b(), key.a(), 1, ws_.data(), s_),
           "fhe_rotate");
     return out;
   }

@@ -93,6 +93,61 @@ int main() {
           }
         }
     }
+    // keys, encryption, rotation and mult+relin+rescale through the C++ layer (§8f): an integer
+    // plaintext m (small coefficients) must decrypt back to m + small noise, and a rotation by
+    // Galois element k to sigma_k(m)
+    {
+      fhe::Context kc = fhe::Context::standard(10, 3, 2, 3);
+      fhe::KeyGenerator kg(kc, 42);
+      const fhe::PublicKey pk = kg.public_key(43);
+      fhe::Evaluator kev(kc);
+      const u64 kn = kc.n();
+      std::vector<u64> kq(5);
+      fhe::check(fhe_ctx_moduli(kc.get(), kq.data(), nullptr), "moduli");
+      std::vector<int64_t> m(kn);
+      for (u64 i = 0; i < kn; ++i) m[i] = (int64_t)(rng() % 2001) - 1000;
+      std::vector<u64> hp(3 * kn);
+      for (uint32_t l = 0; l < 3; ++l)
+        for (u64 i = 0; i < kn; ++i) hp[l * kn + i] = m[i] >= 0 ? (u64)m[i] : kq[l] - (u64)(-m[i]);
+      fhe::Ciphertext pt(kc, 1, 3, false);
+      pt.buf.upload(hp);
+      kev.ntt(pt);
+      const fhe::Ciphertext ct = kev.encrypt(pt, pk, 44);
+      auto decrypt_limb0 = [&](const fhe::Ciphertext& c) {
+        fhe::Ciphertext d = kev.decrypt(c, kg.secret());
+        kev.intt(d);
+        const std::vector<u64> hd = d.buf.download();
+        std::vector<int64_t> r(kn);
+        for (u64 i = 0; i < kn; ++i) {
+          const u64 v = hd[i];  // limb 0
+          r[i] = v > kq[0] / 2 ? -(int64_t)(kq[0] - v) : (int64_t)v;
+        }
+        return r;
+      };
+      const std::vector<int64_t> back = decrypt_limb0(ct);
+      for (u64 i = 0; i < kn; ++i)
+        if (std::llabs(back[i] - m[i]) > 1000) {
+          std::printf("FAIL encrypt/decrypt coeff %llu\n", (unsigned long long)i);
+          return 1;
+        }
+      const uint32_t k = kev.galois_elt(1);
+      const fhe::SwitchKey rk = kg.rotation_key(k, 45);
+      const std::vector<int64_t> r2 = decrypt_limb0(kev.rotate(ct, k, rk));
+      for (u64 i = 0; i < kn; ++i) {
+        const u64 t = i * k % (2 * kn);  // sigma_k moves coefficient i to i k mod 2N (negated past N)
+        const int64_t want = t < kn ? m[i] : -m[i];
+        if (std::llabs(r2[t % kn] - want) > 1000) {
+          std::printf("FAIL rotation coeff %llu\n", (unsigned long long)i);
+          return 1;
+        }
+      }
+      const fhe::SwitchKey rl = kg.relin_key(46);
+      const fhe::Ciphertext sq = kev.mul_relin(ct, ct, rl, false);
+      if (sq.limbs != 3) {
+        std::printf("FAIL mul_relin shape\n");
+        return 1;
+      }
+    }
     std::printf("cpp api ok\n");
     return 0;
   } catch (const fhe::Error& e) {
