@@ -118,6 +118,27 @@ __device__ __forceinline__ u64 shoup_q3(u64 y, u64 w, u64 ws, u64 nq) {
   return ((u64)hi << 32) | (u32)t;
 }
 
+// u + y * w mod q up to two q (the forward CT butterfly's sum output, shoup_q3 with the X-operand
+// folded in): lo64(u + y w + h nq) -- the addend rides in the first mad of the remainder chain, so
+// the sum costs no separate 64-bit add.  Exact as long as the true value u + (y w - h q) < 2^64.
+__device__ __forceinline__ u64 shoup_q3_add(u64 y, u64 w, u64 ws, u64 nq, u64 u) {
+  const u32 y0 = (u32)y, y1 = (u32)(y >> 32);
+  const u32 s0 = (u32)ws, s1 = (u32)(ws >> 32);
+  const u64 a = (u64)y1 * s0;
+  u64 b;
+  u64 cmask;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(b), "=s"(cmask) : "v"(y0), "v"(s1), "v"(a));
+  u32 c;
+  asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(c) : "s"(cmask));
+  const u64 h = mad_u64_u32(y1, s1, ((u64)c << 32) | (u32)(b >> 32));
+  const u32 w0 = (u32)w, w1 = (u32)(w >> 32), n0 = (u32)nq, n1 = (u32)(nq >> 32);
+  const u32 h0 = (u32)h, h1 = (u32)(h >> 32);
+  u64 t = mad_u64_u32(h0, n0, mad_u64_u32(y0, w0, u));
+  FHE_OPAQUE(t);
+  const u32 hi = (u32)(t >> 32) + y1 * w0 + y0 * w1 + h1 * n0 + h0 * n1;
+  return ((u64)hi << 32) | (u32)t;
+}
+
 // a - b + k for a + k > b, with kp1 = k + 1: a + k + 1 + ~b, two 64-bit adds, no borrow chain.
 __device__ __forceinline__ u64 sub_plus(u64 a, u64 b, u64 kp1) {
   u64 nb = ~b;

@@ -61,6 +61,11 @@ constexpr int kColThreads = FHE_COL_THREADS;
 #ifndef FHE_BFLY
 #define FHE_BFLY 2
 #endif
+// FHE_FOLD_U: the forward CT butterfly folds its X-operand into the product's remainder chain
+// (shoup_q3_add): one 64-bit add fewer per butterfly.
+#ifndef FHE_FOLD_U
+#define FHE_FOLD_U 1
+#endif
 #ifndef FHE_HM_POLY_MAJOR
 #define FHE_HM_POLY_MAJOR 1
 #endif
@@ -236,6 +241,29 @@ struct TwSlots {
   static constexpr Tab T = make();
 };
 
+// Twiddle load through an explicitly global pointer: the opaque-base asm in pass_run hides the
+// address space, and a flat load would also count against lgkmcnt, making every LDS wait of the
+// round wait for the twiddles too.
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ ulonglong2 ld_tw(const ulonglong2* p) {
+  const u64x2_t v = *(const __attribute__((address_space(1))) u64x2_t*)p;
+  return make_ulonglong2(v.x, v.y);
+}
+
+// Conditional subtraction in the butterflies.  FHE_CSUB_FAST = 1: sign-mask select (csub_fast:
+// one 64-bit add, an arithmetic shift and two v_bfi, no VCC) instead of a 64-bit compare, two
+// v_cndmask and a borrow chain.  Needs |x - m| < 2^63, which every lazy range here satisfies.
+#ifndef FHE_CSUB_FAST
+#define FHE_CSUB_FAST 1
+#endif
+__device__ __forceinline__ u64 csubk(u64 x, u64 m) {
+#if FHE_CSUB_FAST
+  return csub_fast(x, 0 - m);
+#else
+  return csub(x, m);
+#endif
+}
+
 struct NoHook {
   __device__ __forceinline__ void operator()() const {}
 };
@@ -278,7 +306,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       constexpr int st = LOGR - 1 - bitpos;
       if constexpr (!(FIN == kFinalInv && st == 0)) {  // the last inverse stage folds N^-1 instead
         const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(TS::T.rep_j[sl]) >> (bitpos + 1));
-        tws[sl] = tw[(base << st) + g];
+        tws[sl] = ld_tw(tw + (base << st) + g);
       }
     });
     asm volatile("" ::: "memory");
@@ -287,7 +315,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
   auto twiddle = [&](int b, int j, int bitpos, int st) {
     if constexpr (GATHER) return tws[TS::T.slot[b][j]];
     const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(j) >> (bitpos + 1));
-    return tw[(base << st) + g];
+    return ld_tw(tw + (base << st) + g);
   };
   const u64 q2 = 2 * q, nq = 0 - q;
   [[maybe_unused]] const u64 nq2 = 0 - q2, q2p1 = q2 + 1;
@@ -312,10 +340,22 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
         const ulonglong2 w = twiddle(b, j, bitpos, st);
-        const u64 u = reduce ? csub(x[j], qh) : x[j];
+#if FHE_FOLD_U
+        u64 u = reduce ? csubk(x[j], qh) : x[j];
+        FHE_OPAQUE(u);  // keeps 2u + 3q one v_lshl_add_u64 (not distributed over the select)
+        // u + v straight out of the remainder chain; u - v + 3q = (2u + 3q) - (u + v)
+        u64 s = shoup_q3_add(x[jj], w.x, w.y, nq, u);
+        FHE_OPAQUE(s);
+        x[j] = s;
+        u64 t2 = (u << 1) + q3;
+        FHE_OPAQUE(t2);
+        x[jj] = t2 - s;
+#else
+        const u64 u = reduce ? csubk(x[j], qh) : x[j];
         const u64 v = shoup_q3(x[jj], w.x, w.y, nq);
         x[j] = u + v;
         x[jj] = u - v + q3;
+#endif
       }
     });
     if constexpr (FIN == kFinalFwd || FIN == kFinalFwd2) {
@@ -326,7 +366,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       for (int j = 0; j < E; ++j) {
         static_for<0, 5>([&](auto ci) {
           constexpr int c = 16 >> decltype(ci)::value;  // 16, 8, 4, 2, 1
-          if constexpr (c >= stop && c < rout) x[j] = csub(x[j], (u64)c * q);
+          if constexpr (c >= stop && c < rout) x[j] = csubk(x[j], (u64)c * q);
         });
       }
     }
@@ -384,8 +424,8 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         if (FIN == kFinalInv && st == 0) {
           // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
 #if FHE_BFLY == 2
-          x[j] = csub(csub(shoup_q3(sum, nf0.x, nf0.y, nq), q2), q);
-          x[jj] = csub(csub(shoup_q3(dif, nf1.x, nf1.y, nq), q2), q);
+          x[j] = csubk(csubk(shoup_q3(sum, nf0.x, nf0.y, nq), q2), q);
+          x[jj] = csubk(csubk(shoup_q3(dif, nf1.x, nf1.y, nq), q2), q);
 #else
           x[j] = csub(shoup_lazy(sum, nf0.x, nf0.y, q), q);
           x[jj] = csub(shoup_lazy(dif, nf1.x, nf1.y, q), q);
@@ -393,7 +433,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         } else {
           const ulonglong2 w = twiddle(b, j, bitpos, st);
 #if FHE_BFLY == 2
-          x[j] = csub(sum, q3);
+          x[j] = csubk(sum, q3);
           x[jj] = shoup_q3(dif, w.x, w.y, nq);
 #elif FHE_BFLY == 1
           x[j] = csub_fast(sum, nq2);
@@ -421,6 +461,11 @@ constexpr bool contiguous16() {
 // `base` is wave-uniform and `lane` the per-lane element offset, so every access is an SGPR base
 // (the position's constant part folded in by the scalar unit) plus one 32-bit VGPR offset: no
 // per-element 64-bit address registers.
+// (Accesses go through explicitly global pointers: when the base pointer comes out of an item
+// decode the compiler may lose its address space and emit flat accesses, which also count against
+// lgkmcnt and so make every LDS wait wait for them.)
+using gptr_u64 = __attribute__((address_space(1))) u64*;
+using gptr_u128 = __attribute__((address_space(1))) u64x2_t*;
 template <int STRIDE>
 struct GView {
   u64* base;
@@ -429,28 +474,28 @@ struct GView {
   __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
     const u32 off = lane + tp * STRIDE;
     if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
-      const ulonglong2* v = reinterpret_cast<const ulonglong2*>(base + off);
+      const gptr_u128 v = (gptr_u128)(base + off);
 #pragma unroll
       for (int j = 0; j < kE / 2; ++j) {
-        const ulonglong2 w = v[j];
+        const u64x2_t w = v[j];
         x[2 * j] = w.x;
         x[2 * j + 1] = w.y;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) x[j] = (base + (u64)Lay::jpos(j) * STRIDE)[off];
+      for (int j = 0; j < kE; ++j) x[j] = ((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE))[off];
     }
   }
   template <class Lay>
   __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
     const u32 off = lane + tp * STRIDE;
     if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
-      ulonglong2* v = reinterpret_cast<ulonglong2*>(base + off);
+      const gptr_u128 v = (gptr_u128)(base + off);
 #pragma unroll
-      for (int j = 0; j < kE / 2; ++j) v[j] = make_ulonglong2(x[2 * j], x[2 * j + 1]);
+      for (int j = 0; j < kE / 2; ++j) v[j] = u64x2_t{x[2 * j], x[2 * j + 1]};
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) (base + (u64)Lay::jpos(j) * STRIDE)[off] = x[j];
+      for (int j = 0; j < kE; ++j) ((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE))[off] = x[j];
     }
   }
 };

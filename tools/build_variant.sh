@@ -8,7 +8,7 @@ out=$root/tools/variants/$name; mkdir -p $out
 for f in context.cpp capi.cpp prof.cpp ntt.hip elementwise.hip rns.hip galois.hip serialize.cpp pipeline.hip keygen.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $defs -c $root/gpu-fhe_amd/csrc/$f -o $out/$f.o &
 done
-wait
+wait || exit 1
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $root/tools/variants/$name.so $out/*.o
 rm -rf $out
 echo built tools/variants/$name.so
