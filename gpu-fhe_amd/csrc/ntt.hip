@@ -66,6 +66,11 @@ constexpr int kColThreads = FHE_COL_THREADS;
 #ifndef FHE_FOLD_U
 #define FHE_FOLD_U 1
 #endif
+// FHE_SUB_NOT: the butterflies' 64-bit subtractions as a + k + 1 + ~b (two v_not + one
+// v_lshl_add_u64) instead of a v_sub_co/v_subb_co borrow chain through VCC (2 wait states).
+#ifndef FHE_SUB_NOT
+#define FHE_SUB_NOT 0
+#endif
 #ifndef FHE_HM_POLY_MAJOR
 #define FHE_HM_POLY_MAJOR 1
 #endif
@@ -176,12 +181,16 @@ __device__ __forceinline__ void lds_sync() {
 // read traffic of hm_row_tensor at 8 limbs).  Workgroups are dealt round-robin to the 8 XCDs, so
 // tying the limb to blockIdx % 8 keeps each limb's table on one XCD's L2.  Placement only
 // affects speed: every (limb, rest) pair is still covered exactly once for any nlimbs.
-__device__ __forceinline__ void xcd_limb_split(u32 b, u32 nlimbs, u32& limb, u32& rest) {
+// With more than 8 limbs an XCD owns nlimbs / 8 of them and walks them one after another (the limb
+// changes every `per_limb` = items / nlimbs of its blocks), so only one limb's table is hot in its
+// L2 at a time.
+__device__ __forceinline__ void xcd_limb_split(u32 b, u32 nlimbs, u32 per_limb, u32& limb,
+                                               u32& rest) {
   constexpr u32 kXcd = 8;
   if (nlimbs % kXcd == 0) {
-    const u32 g = nlimbs / kXcd, hi = b / kXcd;
-    limb = b % kXcd + kXcd * (hi % g);
-    rest = hi / g;
+    const u32 hi = b / kXcd;
+    limb = b % kXcd + kXcd * (hi / per_limb);
+    rest = hi % per_limb;
   } else if (kXcd % nlimbs == 0) {
     const u32 per = kXcd / nlimbs;  // XCDs per limb
     limb = (b % kXcd) % nlimbs;
@@ -347,9 +356,13 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         u64 s = shoup_q3_add(x[jj], w.x, w.y, nq, u);
         FHE_OPAQUE(s);
         x[j] = s;
+#if FHE_SUB_NOT
+        x[jj] = sub_plus(u << 1, s, q3 + 1);  // 2u + 3q + 1 + ~s: no borrow chain, no VCC hazard
+#else
         u64 t2 = (u << 1) + q3;
         FHE_OPAQUE(t2);
         x[jj] = t2 - s;
+#endif
 #else
         const u64 u = reduce ? csubk(x[j], qh) : x[j];
         const u64 v = shoup_q3(x[jj], w.x, w.y, nq);
@@ -414,7 +427,11 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         const u64 u = x[j], v = x[jj];
 #if FHE_BFLY == 2
         // GS: inputs in [0, 3q); sum -> [0, 3q); (u - v + 3q) w -> [0, 3q)
+#if FHE_SUB_NOT
+        const u64 sum = u + v, dif = sub_plus(u, v, q3 + 1);
+#else
         const u64 sum = u + v, dif = u - v + q3;
+#endif
 #elif FHE_BFLY == 1
         const u64 sum = u + v, dif = sub_plus(u, v, q2p1);
 #else
@@ -716,7 +733,7 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
   };
   auto decode = [&](u32 it) {
     u32 l, rest;
-    xcd_limb_split(it, nlimbs, l, rest);
+    xcd_limb_split(it, nlimbs, items / nlimbs, l, rest);
     const u32 p = rest % polys, tile = rest / polys;
     const u32 row0 = tile * G::SUBS_R;
     const u64 loc = (u64)l * N + (u64)row0 * G::R2;
@@ -790,7 +807,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[H::ROWS * H::ROWW];
   u32 l, rest;
-  xcd_limb_split(blockIdx.x, nlimbs, l, rest);
+  xcd_limb_split(blockIdx.x, nlimbs, gridDim.x / nlimbs, l, rest);
   // ciphertext fastest: consecutive workgroups of one XCD reuse a row's twiddles while hot
   const u32 batch = gridDim.x / (nlimbs * H::TILES);
   const u32 b = rest % batch, tile = rest / batch;

@@ -42,7 +42,10 @@ def ctx_for(fc, log_n, L, K=0, dnum=1):
 # ------------------------------------------------------------------------------------ NTT
 
 @pytest.mark.parametrize("log_n,L,polys", [(10, 3, 2), (11, 2, 1), (12, 1, 3), (13, 2, 1),
-                                           (14, 4, 2), (15, 2, 1), (16, 8, 2), (17, 4, 1)])
+                                           (14, 4, 2), (15, 2, 1), (16, 8, 2), (17, 4, 1),
+                                           # many limbs (XCD placement walks limbs in runs),
+                                           # incl. the BASELINE configs[4] shape (N=2^17, 32 limbs)
+                                           (13, 24, 3), (14, 12, 2), (16, 16, 1), (17, 32, 1)])
 def test_ntt_matches_oracle(fc, log_n, L, polys):
     ctx = ctx_for(fc, log_n, L)
     x = rand(ctx.moduli, log_n, (polys,), seed=log_n)
@@ -174,6 +177,16 @@ def test_hommult_config3_matches_oracle(fc):
     ctx = ctx_for(fc, 16, 8)
     a = rand(ctx.moduli, 16, (2, 2), seed=21)
     b = rand(ctx.moduli, 16, (2, 2), seed=22)
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    assert (d == coracle.hommult(a, b, ctx.moduli)).all()
+
+
+@pytest.mark.parametrize("log_n,L,B", [(12, 16, 3), (13, 24, 2)])
+def test_hommult_many_limbs_matches_oracle(fc, log_n, L, B):
+    """More limbs than XCDs: the fused row kernel walks each XCD's limbs one after another."""
+    ctx = ctx_for(fc, log_n, L)
+    a = rand(ctx.moduli, log_n, (B, 2), seed=23)
+    b = rand(ctx.moduli, log_n, (B, 2), seed=24)
     d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
     assert (d == coracle.hommult(a, b, ctx.moduli)).all()
 
