@@ -74,6 +74,10 @@ int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 pol
 // the same with separate source / destination poly strides
 int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
                        u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
+// Row pass only, from ntt_row_e8.hip (ntt.hip rebuilt with 8 elements per thread): the second
+// pass of a forward / first pass of an inverse standalone NTT.
+int launch_ntt_row_e8(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
+                      u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
 // Fused ct x ct tensor: a, b [batch][2][nlimbs][N] coefficient form -> d [batch][3][nlimbs][N].
 int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                    u32 nlimbs, void* ws, hipStream_t s);

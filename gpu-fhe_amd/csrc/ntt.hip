@@ -938,6 +938,40 @@ dim3 item_grid(const fhe_ctx* c, int threads, u64 items) {
   return dim3((u32)g);
 }
 
+// Row pass of a standalone NTT over [polys][nlimbs][N] (src poly stride sp -> dst stride dp).
+template <int LOGN, int HD>
+void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 dp, u32 polys,
+              u32 limb0, u32 nlimbs, hipStream_t s) {
+  using G = Geo<LOGN>;
+  const u64 ir = (u64)polys * nlimbs * G::TILES_R;
+  const PolyMap pm{1, sp, 0, dp, 0, 0};
+  if (fwd)
+    k_ntt_row<LOGN, true, HD><<<item_grid<k_ntt_row<LOGN, true, HD>, kLoopRow>(c, G::THR_R, ir),
+                                G::THR_R, 0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir,
+                                                  c->d_tw_fwd, c->d_mods);
+  else
+    k_ntt_row<LOGN, false><<<item_grid<k_ntt_row<LOGN, false>, kLoopRow>(c, G::THR_R, ir),
+                             G::THR_R, 0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv,
+                                               c->d_mods);
+}
+
+#if !FHE_NTT_ROW_ONLY
+// FHE_ROW_E8: the standalone row passes come from ntt_row_e8.hip, this file rebuilt with E = 8
+// elements per thread (half the VGPRs and LDS per wave: twice the resident waves to hide the row
+// twiddles' L2 latency; measured row-forward -9 %, row-inverse -2 %).  The fused HomMult kernel
+// and the column passes keep E = 16 (the fused kernel is 21 % slower at E = 8).
+#ifndef FHE_ROW_E8
+#define FHE_ROW_E8 1
+#endif
+template <int LOGN, int HD>
+void row_pass_any(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 dp,
+                  u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
+  if (FHE_ROW_E8)
+    launch_ntt_row_e8(c, fwd, src, sp, dst, dp, polys, limb0, nlimbs, s);
+  else
+    row_pass<LOGN, HD>(c, fwd, src, sp, dst, dp, polys, limb0, nlimbs, s);
+}
+
 template <int LOGN, int HD>
 int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* dst,
                  u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
@@ -946,17 +980,15 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   const PolyMap pm{1, spstride, 0, dpstride, 0, 0};
   // the second pass runs in place on dst
   const PolyMap pd = flat_map(dpstride);
-  const u64 ic = pl * G::TILES_C, ir = pl * G::TILES_R;
+  const u64 ic = pl * G::TILES_C;
   if (fwd) {
     k_ntt_col<LOGN, true, HD><<<item_grid<k_ntt_col<LOGN, true, HD>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
         src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd, c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_fwd");
-    k_ntt_row<LOGN, true, HD><<<item_grid<k_ntt_row<LOGN, true, HD>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
-        dst, dst, nlimbs, limb0, pd, (u32)ir, c->d_tw_fwd, c->d_mods);
+    row_pass_any<LOGN, HD>(c, true, dst, dpstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_fwd");
   } else {
-    k_ntt_row<LOGN, false><<<item_grid<k_ntt_row<LOGN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R, 0, s>>>(
-        src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv, c->d_mods);
+    row_pass_any<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_inv");
     k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, false>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
         dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv, c->d_nfold, c->d_mods);
@@ -994,10 +1026,30 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;
 }
+#endif  // !FHE_NTT_ROW_ONLY
 
 }  // namespace
 
 #define FHE_LOGN_CASES(X) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17)
+
+#if FHE_NTT_ROW_ONLY
+int launch_ntt_row_e8(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
+                      u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
+  switch (c->log_n) {
+#define X(n)                                                                                  \
+  case n:                                                                                     \
+    if (c->lz16)                                                                              \
+      row_pass<n, 16>(c, forward, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);    \
+    else                                                                                      \
+      row_pass<n, 8>(c, forward, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);     \
+    return kOk;
+    FHE_LOGN_CASES(X)
+#undef X
+  }
+  set_error("unsupported log_n");
+  return kUnsupported;
+}
+#else
 
 int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 polys, u64 pstride,
                u32 limb0, u32 nlimbs, hipStream_t s) {
@@ -1071,5 +1123,7 @@ int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 bat
   FHE_HIP_CHECK(hipStreamWaitEvent(s, cc->aux_join, 0));
   return kOk;
 }
+
+#endif  // FHE_NTT_ROW_ONLY
 
 }  // namespace fhe
