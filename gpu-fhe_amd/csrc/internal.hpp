@@ -78,6 +78,25 @@ int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstr
 // pass of a forward / first pass of an inverse standalone NTT.
 int launch_ntt_row_e8(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
                       u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
+// Column-forward pass only (first half of a forward NTT; the key-switch's fused row kernel
+// finishes it).
+int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
+                       u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
+// Fused key-switch row kernel (ntt.hip, k_ks_row_inner): row-forward NTT of every ModUp digit's
+// column-passed rows + inner product with the key.  ext [dnum][batch][rows][N] (digit stride
+// ext_ds words), d2_own [batch][nq][N] NTT form, evk [dnum][rows][N], acc [2][batch][rows][N]
+// (second half at acc + acc_ws); row r -> limb r < nq ? base0 + r : base1 + r - nq.
+struct KsRowArgs {
+  u64* acc;
+  u64 acc_ws;
+  const u64* ext;
+  u64 ext_ds;
+  const u64* d2_own;
+  const u64* evk_b;
+  const u64* evk_a;
+  u32 rows, nq, base0, base1, alpha, L, batch;
+};
+int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s);
 // Fused ct x ct tensor: a, b [batch][2][nlimbs][N] coefficient form -> d [batch][3][nlimbs][N].
 int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                    u32 nlimbs, void* ws, hipStream_t s);

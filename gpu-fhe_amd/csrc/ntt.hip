@@ -913,6 +913,136 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   });
 }
 
+// Fused key-switch row kernel: the row-forward NTT of every ModUp digit plus the inner product
+// with the evaluation key, so the extended digits never go back to HBM in NTT form and no separate
+// inner-product pass re-reads them (SURVEY §8a' key-switch; the unfused path is k_ntt_row per digit
+// + k_ks_inner in rns.hip).  Workgroup = (row r of Q u P, ciphertext b, tile of H::ROWS rows of the
+// R1 x R2 view); thread group g = digit j (whole wavefronts, as in k_hommult_row):
+//   * if row r's limb belongs to digit j, its value is d2 itself: the NTT-form d2_own row, loaded;
+//   * else ext_j's column-forward row: the row-forward stages run in registers / LDS, with no
+//     final reduction (the products are accumulated as 128-bit integers, any 64-bit operand);
+// all digits publish to LDS slot j; then every thread combines 4 of its 16 positions for both
+// outputs: acc{0,1} = sum_j x_j * evk{b,a}[j][r] (128-bit sums of DNUM products, one reduce128).
+// Rows: r < nq -> own Q-limb base0 + r, else special limb base1 + (r - nq).
+template <int LOGN, int HR, int DNUM>
+__global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
+                                         const u64* __restrict__ ext, u64 ext_ds,
+                                         const u64* __restrict__ d2_own,
+                                         const u64* __restrict__ evk_b,
+                                         const u64* __restrict__ evk_a, u32 rows, u32 nq,
+                                         u32 base0, u32 base1, u32 alpha, u32 L, u32 batch,
+                                         const ulonglong2* __restrict__ twf,
+                                         const ModParams* __restrict__ mods) {
+  static_assert(DNUM >= 1 && DNUM <= 4, "one thread group per digit, four groups");
+  using G = Geo<LOGN>;
+  using H = HmGeo<LOGN>;
+  using Rd = Rounds<G::N2>;
+  constexpr u64 N = 1ull << LOGN;
+  __shared__ u64 lds[H::ROWS * H::ROWW];
+  // XCD-major placement, ciphertext fastest: the workgroups of one XCD run all `batch` ciphertexts
+  // of a (row, tile) back to back, so that tile's key words and twiddles are read from HBM once
+  // and served from that XCD's L2 for the rest (gridDim.x = rows * TILES * batch, TILES % 8 == 0)
+  u32 b, r, tile;
+  if ((rows * H::TILES) % 8 == 0) {
+    const u32 xcd = blockIdx.x % 8, k8 = blockIdx.x / 8;
+    const u32 rt = xcd + 8 * (k8 / batch);
+    b = k8 % batch;
+    r = rt % rows;
+    tile = rt / rows;
+  } else {  // small N: too few tiles to deal out by XCD
+    r = blockIdx.x % rows;
+    b = (blockIdx.x / rows) % batch;
+    tile = blockIdx.x / (rows * batch);
+  }
+  const u32 limb = r < nq ? base0 + r : base1 + (r - nq);
+  const ModParams m = mods[limb];
+  const u64 q = m.q;
+  const u64 rn = (u64)rows * N;
+  // digit-major thread groups (whole wavefronts), as k_hommult_row's poly-major layout
+  const u32 grp = __builtin_amdgcn_readfirstlane(threadIdx.x / (H::ROWS * H::TPS));
+  const u32 sub = (threadIdx.x / H::TPS) % H::ROWS, t = threadIdx.x % H::TPS;
+  const u32 row = tile * H::ROWS + sub;
+  const u64 loc = (u64)row * G::R2;
+  const u32 base = (u32)G::R1 + row;
+  u64* rowlds = lds + sub * H::ROWW;
+  const LView<1, true> own_slot{rowlds + grp * G::RS};
+  constexpr int SY = H::SYNC_ROUND;
+  using LayT = Layout<G::N2, Rd::kb(Rd::NR - 1), Rd::lo_fwd(Rd::NR - 1)>;
+  const u32 tpT = LayT::tpos(t);
+  const bool is_own = limb < L && grp == limb / alpha;  // wave-uniform
+  u64 v[kE];
+  if (grp < (u32)DNUM) {
+    if (is_own) {
+      const GView<1> gin{const_cast<u64*>(d2_own) + ((u64)b * nq + r) * N + loc, 0};
+      gin.template load<LayT>(v, tpT);
+    } else {
+      const ulonglong2* tf = twf + (u64)limb * N;
+      static_for<0, Rd::NR>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int KB = Rd::kb(k);
+        constexpr int LO = Rd::lo_fwd(k);
+        constexpr int RIN = fwd_range(fwd_range(1, G::N1, HR), G::N2 - (LO + KB), HR);
+        using Lay = Layout<G::N2, KB, LO>;
+        const u32 tp = Lay::tpos(t);
+        if constexpr (k == 0) {
+          const GView<1> gin{const_cast<u64*>(ext) + (u64)grp * ext_ds + (u64)b * rn + (u64)r * N + loc, 0};
+          gin.template load<Lay>(v, tp);
+        } else {
+          lds_sync<SY>();
+          own_slot.template load<Lay>(v, tp);
+        }
+        round_compute<G::N2, KB, LO, true, kNotFinal, true, HR, RIN>(v, tp, tf, base, q, {0, 0},
+                                                                     {0, 0});
+        if constexpr (k < Rd::NR - 1) {
+          if (k > 0) lds_sync<SY>();
+          own_slot.template store<Lay>(v, tp);
+        }
+      });
+    }
+    lds_sync<SY>();
+    own_slot.template store<LayT>(v, tpT);
+  }
+  __syncthreads();
+  // combine: the workgroup's ROWS x R2 positions are re-dealt so that each thread takes CW
+  // consecutive positions of one row and a wavefront covers contiguous words (coalesced 16-byte
+  // key loads and output stores)
+  constexpr int CW = (H::ROWS * G::R2) / H::THR;
+  static_assert(CW == 4 || CW == 2 || CW == 8, "combine width");
+  const u32 cpos0 = threadIdx.x * CW;
+  const u32 crow = cpos0 / G::R2, cpos = cpos0 % G::R2;
+  const u64 okey = (u64)r * N + (u64)(tile * H::ROWS + crow) * G::R2 + cpos;
+  const u64* lrow = lds + crow * H::ROWW;
+  u64 o0[CW], o1[CW];
+#pragma unroll
+  for (int e = 0; e < CW; e += 2) {
+    u128 s0[2] = {0, 0}, s1[2] = {0, 0};
+#pragma unroll
+    for (int d = 0; d < DNUM; ++d) {
+      const u64x2_t kb = *(const __attribute__((address_space(1))) u64x2_t*)(evk_b + (u64)d * rn + okey + e);
+      const u64x2_t ka = *(const __attribute__((address_space(1))) u64x2_t*)(evk_a + (u64)d * rn + okey + e);
+      const u32 p = cpos + e;
+      const u64 x0 = lrow[d * G::RS + p + (p >> 4)];
+      const u64 x1 = lrow[d * G::RS + (p + 1) + ((p + 1) >> 4)];
+      s0[0] += (u128)x0 * kb.x;
+      s0[1] += (u128)x1 * kb.y;
+      s1[0] += (u128)x0 * ka.x;
+      s1[1] += (u128)x1 * ka.y;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      o0[e + h] = reduce128((u64)s0[h], (u64)(s0[h] >> 64), m);
+      o1[e + h] = reduce128((u64)s1[h], (u64)(s1[h] >> 64), m);
+    }
+  }
+  gptr_u128 a0 = (gptr_u128)(acc + (u64)b * rn + okey);
+  gptr_u128 a1 = (gptr_u128)(acc + acc_ws + (u64)b * rn + okey);
+#pragma unroll
+  for (int e = 0; e < CW; e += 2) {
+    a0[e / 2] = u64x2_t{o0[e], o0[e + 1]};
+    a1[e / 2] = u64x2_t{o1[e], o1[e + 1]};
+  }
+}
+
 // One-generation grid for an item-loop kernel: as many workgroups as fit on the device at once
 // (occupancy queried once per kernel), never more than the items, rounded up to a multiple of 8
 // so item -> XCD placement holds (surplus workgroups exit at once).
@@ -1050,6 +1180,72 @@ int launch_ntt_row_e8(const fhe_ctx* c, bool forward, const u64* src, u64 spstri
   return kUnsupported;
 }
 #else
+
+namespace {
+template <int LOGN, int HD>
+void col_fwd_pass(const fhe_ctx* c, const u64* src, u64 sp, u64* dst, u64 dp, u32 polys,
+                  u32 limb0, u32 nlimbs, hipStream_t s) {
+  using G = Geo<LOGN>;
+  const u64 ic = (u64)polys * nlimbs * G::TILES_C;
+  const PolyMap pm{1, sp, 0, dp, 0, 0};
+  k_ntt_col<LOGN, true, HD><<<item_grid<k_ntt_col<LOGN, true, HD>, kLoopCol>(c, G::THR_C, ic),
+                              G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic,
+                                                c->d_tw_fwd, c->d_nfold, c->d_mods);
+}
+
+template <int LOGN, int HD>
+int ks_row_inner_dispatch(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
+  using H = HmGeo<LOGN>;
+  const dim3 g((u32)((u64)a.rows * a.batch * H::TILES));
+  switch (c->dnum) {
+#define D(k)                                                                                    \
+  case k:                                                                                       \
+    k_ks_row_inner<LOGN, HD, k><<<g, H::THR, 0, s>>>(                                           \
+        a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.base0,   \
+        a.base1, a.alpha, a.L, a.batch, c->d_tw_fwd, c->d_mods);                               \
+    break;
+    D(1) D(2) D(3) D(4)
+#undef D
+    default:
+      set_error("ks_row_inner: dnum > 4");
+      return kUnsupported;
+  }
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+}  // namespace
+
+int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
+                       u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
+  if ((u64)polys * nlimbs == 0) return kOk;
+  switch (c->log_n) {
+#define X(n)                                                                                 \
+  case n:                                                                                    \
+    if (c->lz16)                                                                             \
+      col_fwd_pass<n, 16>(c, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);        \
+    else                                                                                     \
+      col_fwd_pass<n, 8>(c, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);         \
+    FHE_HIP_CHECK(hipGetLastError());                                                       \
+    return kOk;
+    FHE_LOGN_CASES(X)
+#undef X
+  }
+  set_error("unsupported log_n");
+  return kUnsupported;
+}
+
+int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
+  if ((u64)a.rows * a.batch == 0) return kOk;
+  switch (c->log_n) {
+#define X(n) \
+  case n:    \
+    return c->lz16 ? ks_row_inner_dispatch<n, 16>(c, a, s) : ks_row_inner_dispatch<n, 8>(c, a, s);
+    FHE_LOGN_CASES(X)
+#undef X
+  }
+  set_error("unsupported log_n");
+  return kUnsupported;
+}
 
 int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 polys, u64 pstride,
                u32 limb0, u32 nlimbs, hipStream_t s) {

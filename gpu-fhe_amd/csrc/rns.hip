@@ -19,6 +19,9 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxSrc = 16;
+#ifndef FHE_KS_FUSED
+#define FHE_KS_FUSED 1
+#endif
 
 // out row r -> ctx limb: r < n0 ? base0 + r : base1 + (r - n0)
 struct RowMap {
@@ -37,6 +40,12 @@ inline ulonglong2 shoup_pair(u64 w, u64 q) {
 // ctx limb map.limb(r); rows whose limb lies in [skip_lo, skip_hi) are left untouched.
 // inv[k] = (S^_k)^-1 mod s_k; hat[k * hs + limb] = S^_k mod limb.  Batch b = blockIdx.y reads
 // in + b * in_bs and writes out + b * out_bs.
+// The launch's conversion constants (S x T Shoup pairs' first words and each row's modulus) are
+// staged in LDS once per workgroup, so the row loop reads broadcast LDS words instead of waiting
+// on a scalar load per row; each output is a 128-bit sum of S full products y_k * (S^_k mod t)
+// (< S t^2 < 2^126), reduced once (Montgomery for S < 8, else reduce128), instead of S Shoup
+// products and S subtractions.
+constexpr int kMaxRows = 64;
 template <int S>
 __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ in, u64 in_bs,
                                                        u32 src0, u64* __restrict__ out, u64 out_bs,
@@ -44,6 +53,18 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
                                                        u64 n, const ulonglong2* __restrict__ inv,
                                                        const ulonglong2* __restrict__ hat, u32 hs,
                                                        const ModParams* __restrict__ mods) {
+  // S < 8: y_k < 2^61 and S 2^61 < 2^64, so the sum stays below t 2^64 and one Montgomery
+  // reduction (R = 2^64, folded into the table's second word) replaces reduce128
+  constexpr bool kMont = S < 8;
+  __shared__ u64 s_hat[kMaxRows * S];
+  __shared__ u32 s_limb[kMaxRows];
+  for (u32 e = threadIdx.x; e < T * S; e += blockDim.x) {
+    const u32 r = e / S, k = e % S;
+    const ulonglong2 h = hat[(u64)k * hs + map.limb(r)];
+    s_hat[e] = kMont ? h.y : h.x;
+  }
+  for (u32 r = threadIdx.x; r < T; r += blockDim.x) s_limb[r] = map.limb(r);
+  __syncthreads();
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   in += (u64)blockIdx.y * in_bs;
@@ -56,16 +77,17 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
     y[k] = csub(shoup_lazy(in[(u64)k * n + i], w.x, w.y, qk), qk);
   }
   for (u32 r = 0; r < T; ++r) {
-    const u32 limb = map.limb(r);
+    const u32 limb = s_limb[r];
     if (limb >= skip_lo && limb < skip_hi) continue;
-    const u64 t = mods[limb].q, t2 = 2 * t;
-    u64 acc = 0;
+    u128 acc = 0;
 #pragma unroll
-    for (int k = 0; k < S; ++k) {
-      const ulonglong2 w = hat[(u64)k * hs + limb];
-      acc = csub(acc + shoup_lazy(y[k], w.x, w.y, t), t2);
+    for (int k = 0; k < S; ++k) acc += (u128)y[k] * s_hat[r * S + k];
+    if constexpr (kMont) {
+      const ModParams& m = mods[limb];
+      out[(u64)r * n + i] = csub(mont_reduce_lazy((u64)acc, (u64)(acc >> 64), m.q, m.qinv), m.q);
+    } else {
+      out[(u64)r * n + i] = reduce128((u64)acc, (u64)(acc >> 64), mods[limb]);
     }
-    out[(u64)r * n + i] = csub(acc, t);
   }
 }
 
@@ -161,7 +183,9 @@ void conv_tables(const std::vector<u64>& mods, u32 s0, u32 S, std::vector<ulongl
       u64 hm = 1;
       for (u32 i = 0; i < S; ++i)
         if (i != k) hm = mulmod_u64(hm, mods[s0 + i] % tm, tm);
-      hat[(size_t)k * M + t] = shoup_pair(hm, tm);
+      // {S^_k mod t, S^_k 2^64 mod t}: the plain word for the 128-bit sums of k_baseconv (S >= 8),
+      // the Montgomery form for its Montgomery-reduced sums (S < 8)
+      hat[(size_t)k * M + t] = ulonglong2{hm, (u64)(((u128)hm << 64) % tm)};
     }
   }
 }
@@ -183,8 +207,20 @@ template <int S>
 void launch_bc(const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* hat, u32 hs,
                const ModParams* mods, hipStream_t s) {
   const dim3 g((u32)((n + kThreads - 1) / kThreads), a.batch);
-  k_baseconv<S><<<g, kThreads, 0, s>>>(a.in, a.in_bs, a.src0, a.out, a.out_bs, a.T, a.map,
-                                       a.skip_lo, a.skip_hi, n, inv, hat, hs, mods);
+  // the kernel stages at most kMaxRows target rows' constants: longer targets go in chunks
+  for (u32 r0 = 0; r0 < a.T; r0 += kMaxRows) {
+    const u32 t = std::min<u32>(kMaxRows, a.T - r0);
+    RowMap m = a.map;
+    if (r0 < m.n0) {
+      m.n0 -= r0;
+      m.base0 += r0;
+    } else {
+      m.base1 += r0 - m.n0;
+      m.n0 = 0;
+    }
+    k_baseconv<S><<<g, kThreads, 0, s>>>(a.in, a.in_bs, a.src0, a.out + (u64)r0 * n, a.out_bs, t,
+                                         m, a.skip_lo, a.skip_hi, n, inv, hat, hs, mods);
+  }
 }
 
 int baseconv_any(u32 S, const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* hat,
@@ -269,6 +305,14 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   const u64 acc_ws = B * rn;
   const RowMap map{nlimbs, limb0, L};
   int rc;
+  // FHE_KS_FUSED: for dnum <= 4 the digits get only their column-forward pass here, and one fused
+  // kernel (ntt.hip, k_ks_row_inner) runs every digit's row-forward pass and the inner product
+  // (no NTT-form ext in HBM, no separate inner-product pass); otherwise full NTTs + k_ks_inner.
+  const bool fused = FHE_KS_FUSED && c->dnum <= 4;
+  auto ntt_fwd = [&](u64* p, u32 l0, u32 nl) {
+    return fused ? launch_ntt_col_fwd(c, p, rn, p, rn, batch, l0, nl, s)
+                 : launch_ntt(c, true, p, p, batch, rn, l0, nl, s);
+  };
   // ModUp + NTT, per digit, for every row outside the digit itself
   for (u32 j = 0; j < c->dnum; ++j) {
     const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
@@ -279,16 +323,19 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
       return rc;
     // own Q-limbs outside [lo, hi): up to two ranges, then the P-limbs
     const u32 a0 = limb0, a1 = std::min(limb0 + nlimbs, lo);
-    if (a1 > a0 && (rc = launch_ntt(c, true, e, e, batch, rn, a0, a1 - a0, s))) return rc;
+    if (a1 > a0 && (rc = ntt_fwd(e, a0, a1 - a0))) return rc;
     const u32 b0 = std::max(limb0, hi), b1 = limb0 + nlimbs;
-    u64* eb = e + (u64)(b0 - limb0) * n;
-    if (b1 > b0 && (rc = launch_ntt(c, true, eb, eb, batch, rn, b0, b1 - b0, s))) return rc;
-    u64* ep = e + (u64)nlimbs * n;
-    if ((rc = launch_ntt(c, true, ep, ep, batch, rn, L, K, s))) return rc;
+    if (b1 > b0 && (rc = ntt_fwd(e + (u64)(b0 - limb0) * n, b0, b1 - b0))) return rc;
+    if ((rc = ntt_fwd(e + (u64)nlimbs * n, L, K))) return rc;
   }
   prof_mark(s, "ks_modup");
+  if (fused) {
+    const KsRowArgs ka{acc, acc_ws, ext, B * rn, d2_own, evk_b, evk_a, rows, nlimbs, limb0, L,
+                       alpha, L, batch};
+    if ((rc = launch_ks_row_inner(c, ka, s))) return rc;
+  }
   const dim3 gi((u32)(n / kThreads), rows);
-  switch (c->dnum) {
+  if (!fused) switch (c->dnum) {
 #define X(k)                                                                                     \
   case k:                                                                                        \
     k_ks_inner<k><<<gi, kThreads, 0, s>>>(acc, acc_ws, ext, d2_own, evk_b, evk_a, rows, nlimbs, \
