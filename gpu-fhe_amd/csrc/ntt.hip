@@ -66,6 +66,13 @@ constexpr int kColThreads = FHE_COL_THREADS;
 #ifndef FHE_FOLD_U
 #define FHE_FOLD_U 1
 #endif
+// FHE_HM_TILED: HomMult's column-forward pass writes its workspace tile-major (one contiguous
+// block per workgroup) and the fused row kernel reads it so (k_ntt_col TILED, TView).  Measured
+// neutral to -2 % (hm_col_fwd 116.5 vs 113.3 us): the 128-byte row segments of the flat layout
+// are not what holds the column pass below the HBM copy rate.  Kept as an A/B switch.
+#ifndef FHE_HM_TILED
+#define FHE_HM_TILED 0
+#endif
 // FHE_SUB_NOT: the butterflies' 64-bit subtractions as a + k + 1 + ~b (two v_not + one
 // v_lshl_add_u64) instead of a v_sub_co/v_subb_co borrow chain through VCC (2 wait states).
 #ifndef FHE_SUB_NOT
@@ -559,6 +566,21 @@ struct LViewC {
   }
 };
 
+// Global view of one row of a tile-major limb (k_ntt_col<..., TILED>): row position c of row
+// `row` lives at base[(c / S) (R1 S) + row S + c % S]; base = the limb's start + row * S.
+template <int S, int R1>
+struct TView {
+  const u64* base;
+  template <class Lay>
+  __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
+#pragma unroll
+    for (int j = 0; j < kE; ++j) {
+      const u32 c = tp | Lay::jpos(j);
+      x[j] = ((gptr_u64)base)[(c / S) * (R1 * S) + c % S];
+    }
+  }
+};
+
 // Round-0 global load of one sub-transform into registers (issued ahead of the work that needs
 // it: the kernels below prefetch their next item while computing the current one).
 template <int LOGR, bool FWD, class GIn>
@@ -658,7 +680,10 @@ struct Geo {
 // multiple of 8, so an item keeps the XCD (blockIdx % 8) its index maps to.
 
 // Column pass over items (p, l, tile) of src/dst [polys][nlimbs][N] via PolyMap.
-template <int LOGN, bool FWD, int H = 8>
+// TILED: dst limb rows are written tile-major -- column tile k (SUBS_C columns x R1 rows) as one
+// contiguous block [k][row][SUBS_C] -- so every workgroup's output is one contiguous run of
+// R1 SUBS_C words (the HomMult workspace; the fused row kernel reads it through TView).
+template <int LOGN, bool FWD, int H = 8, bool TILED = false>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_ntt_col(const u64* __restrict__ src,
                                                       const u64* __restrict__ src2,
@@ -681,8 +706,9 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     const u32 tile = it % G::TILES_C, pl = it / G::TILES_C;
     const u32 l = pl % nlimbs, p = pl / nlimbs;
     const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
+    const u64 dloc = TILED ? (u64)l * N + (u64)tile * G::SUBS_C * G::R1 : loc;
     const u64* s = pm.second(p) ? src2 + pm.src2(p) : src + pm.src(p);
-    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), s + loc, dst + pm.dst(p) + loc};
+    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), s + loc, dst + pm.dst(p) + dloc};
   };
   u32 it = blockIdx.x;
   if (it >= items) return;
@@ -701,8 +727,9 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       nf0 = nfold[4 * cur.limb];
       nf1 = nfold[4 * cur.limb + 1];
     }
+    using GOut = GView<TILED ? G::SUBS_C : G::R2>;
     pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
-        x, GView<G::R2>{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
+        x, GOut{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
         nf0, nf1, prefetch);
     if (!more) break;
     it = nx;
@@ -794,7 +821,7 @@ struct HmGeo {
   static constexpr int SYNC_ROUND = (POLY_MAJOR || LANES_ROW <= 64) ? kWaveSync : kBlockSync;
 };
 
-template <int LOGN, int HR = 8>
+template <int LOGN, int HR = 8, bool TILED = false>
 __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
                                                           u64* __restrict__ d, u32 nlimbs,
                                                           u32 limb0,
@@ -847,8 +874,14 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
     using Lay = Layout<G::N2, KB, LO>;
     const u32 tp = Lay::tpos(t);
     if constexpr (k == 0) {
-      const GView<1> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
-      gin.template load<Lay>(v, tp);
+      if constexpr (TILED) {
+        const TView<G::SUBS_C, G::R1> gin{x + ((u64)b * 4 + grp) * limbN + (u64)l * N +
+                                          (u64)row * G::SUBS_C};
+        gin.template load<Lay>(v, tp);
+      } else {
+        const GView<1> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
+        gin.template load<Lay>(v, tp);
+      }
     } else {
       lds_sync<SY>();
       own.template load<Lay>(v, tp);
@@ -1139,13 +1172,14 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   // over the 4 polys of every ciphertext pair (group of 4: slots 0, 1 from a, slots 2, 3 from b)
   const PolyMap to_x{4, 2 * limbN, limbN, 4 * limbN, limbN, 2};
   const u64 ic = (u64)batch * 4 * nlimbs * G::TILES_C;
-  k_ntt_col<LOGN, true, HD><<<item_grid<k_ntt_col<LOGN, true, HD>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0,
-                          s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic, c->d_tw_fwd, c->d_nfold,
-                               c->d_mods);
+  constexpr bool TL = FHE_HM_TILED != 0;
+  k_ntt_col<LOGN, true, HD, TL><<<item_grid<k_ntt_col<LOGN, true, HD, TL>, kLoopCol>(c, G::THR_C, ic),
+                                  G::THR_C, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic,
+                                                    c->d_tw_fwd, c->d_nfold, c->d_mods);
   prof_mark(s, "hm_col_fwd");
   const dim3 gh((u32)((u64)batch * nlimbs * H::TILES));
-  k_hommult_row<LOGN, HD><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd, c->d_tw_inv,
-                                            c->d_mods);
+  k_hommult_row<LOGN, HD, TL><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd,
+                                                    c->d_tw_inv, c->d_mods);
   prof_mark(s, "hm_row_tensor");
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
