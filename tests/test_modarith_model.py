@@ -92,3 +92,49 @@ def test_lazy_butterfly_ranges(q):
         d = shoup_q3(x - y + 3 * q, w, ws, q)
         assert 0 <= s < 3 * q and 0 <= d < 3 * q
         assert (d - (x - y) * w) % q == 0
+
+
+def shoup_q3_add(y, w, ws, q, u):
+    """modarith.hpp shoup_q3_add: u rides in the first mad of the remainder chain."""
+    y0, y1 = y & M32, y >> 32
+    s0, s1 = ws & M32, ws >> 32
+    a = y1 * s0
+    bfull = y0 * s1 + a
+    b, c = bfull & M64, bfull >> 64
+    h = (y1 * s1 + ((c << 32) | (b >> 32))) & M64
+    nq = (-q) & M64
+    w0, w1, n0, n1 = w & M32, w >> 32, nq & M32, nq >> 32
+    h0, h1 = h & M32, h >> 32
+    t = (h0 * n0 + ((y0 * w0 + u) & M64)) & M64
+    hi = ((t >> 32) + y1 * w0 + y0 * w1 + h1 * n0 + h0 * n1) & M32
+    return (hi << 32) | (t & M32)
+
+
+def csub_fast(x, m):
+    """modarith.hpp csub_fast (sign of x - m selects): valid while |x - m| < 2^63."""
+    d = (x - m) & M64
+    return x if d >> 63 else d
+
+
+@pytest.mark.parametrize("q", _moduli())
+@pytest.mark.parametrize("H", [8, 16])
+def test_folded_ct_butterfly(q, H):
+    """FHE_FOLD_U: outputs u + v (from the chain) and (2u + 3q) - (u + v) mod 2^64 are the exact
+    lazy CT outputs for every X-operand range the compile-time schedule allows (u < (H - 3) q after
+    the optional reduction by H/2 q), at both headrooms (H = 16 needs q < 2^60)."""
+    if H == 16 and q >= 1 << 60:
+        pytest.skip("16q headroom needs q < 2^60")
+    rng = random.Random(q + 3 + H)
+    for _ in range(3000):
+        w = rng.randrange(q)
+        ws = (w << 64) // q
+        y = rng.randrange(H * q)
+        x = rng.randrange(H * q)
+        u = csub_fast(x, (H // 2) * q) if x + 3 * q > H * q else x
+        assert u == (x - (H // 2) * q if x >= (H // 2) * q and x + 3 * q > H * q else x)
+        s = shoup_q3_add(y, w, ws, q, u)
+        v = shoup_q3(y, w, ws, q)
+        assert s == u + v and s < H * q
+        o2 = ((u << 1) + 3 * q - s) & M64
+        assert o2 == u - v + 3 * q and o2 < H * q
+        assert (s - (x + w * y)) % q == 0 and (o2 - (x - w * y)) % q == 0
