@@ -97,6 +97,18 @@ struct KsRowArgs {
   u32 rows, nq, base0, base1, alpha, L, batch;
 };
 int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s);
+// ModUp column pass (ntt.hip, k_modup_col): converts a digit's S pre-scaled source rows
+// y [batch][S][N] into each of its T target rows and runs their column-forward pass, writing the
+// column-passed rows into ext [batch][rows][N] (row stride N, ciphertext stride rn words).
+struct ModUpColArgs {
+  const u64* y;
+  u64* ext;
+  u64 rn;
+  u32 S, T, skip_at, skip_len, n0, base0, base1, batch;
+  const ulonglong2* hat;  // this digit's conversion table: hat[k hs + limb]
+  u32 hs;
+};
+int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s);
 // Fused ct x ct tensor: a, b [batch][2][nlimbs][N] coefficient form -> d [batch][3][nlimbs][N].
 int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                    u32 nlimbs, void* ws, hipStream_t s);

@@ -946,6 +946,66 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   });
 }
 
+// ModUp column pass (key-switch): the column-forward pass of every extended row of one digit,
+// reading its input straight from the digit's S pre-scaled source rows y_k = [x_k (D^_k)^-1]_{d_k}
+// (coefficient form, rns.hip k_modup_scale) and converting on the fly:
+//   x = sum_k y_k (D^_k mod t) mod t   (128-bit sum < S 2^61 t < t 2^64, one Montgomery reduction;
+//                                       hat[k hs + t].y = D^_k 2^64 mod t)
+// so the extended rows are never written in coefficient form (SURVEY §8a' ModUp; the unfused path
+// is k_baseconv + k_ntt_col).  Items (target row, ciphertext, column tile) are dealt XCD-major,
+// target fastest: an XCD converts every target of a (ciphertext, tile) while the S source tiles are
+// hot in its L2.  Target tr -> row r = tr < skip_at ? tr : tr + skip_len (the digit's own rows are
+// skipped) -> limb r < n0 ? base0 + r : base1 + (r - n0).
+template <int LOGN, int H, int S>
+__global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
+    FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_modup_col(const u64* __restrict__ y,
+                                                        u64* __restrict__ ext, u64 rn, u32 T,
+                                                        u32 skip_at, u32 skip_len, u32 n0,
+                                                        u32 base0, u32 base1, u32 batch,
+                                                        const ulonglong2* __restrict__ hat,
+                                                        u32 hs,
+                                                        const ulonglong2* __restrict__ tw_all,
+                                                        const ModParams* __restrict__ mods) {
+  using G = Geo<LOGN>;
+  using Rd = Rounds<G::N1>;
+  using Lay0 = Layout<G::N1, Rd::kb(0), Rd::lo_fwd(0)>;
+  constexpr u64 N = 1ull << LOGN;
+  __shared__ u64 lds[G::LDS_C];
+  const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
+  const LViewC<G::SUBS_C> lv{lds + sub};
+  const u32 nbt = batch * G::TILES_C;
+  u32 tr, bt;
+  if (nbt % 8 == 0) {
+    const u32 xcd = blockIdx.x % 8, k8 = blockIdx.x / 8;
+    tr = k8 % T;
+    bt = xcd + 8 * (k8 / T);
+  } else {
+    tr = blockIdx.x % T;
+    bt = blockIdx.x / T;
+  }
+  const u32 b = bt / G::TILES_C, tile = bt % G::TILES_C;
+  const u32 r = tr < skip_at ? tr : tr + skip_len;
+  const u32 limb = __builtin_amdgcn_readfirstlane(r < n0 ? base0 + r : base1 + (r - n0));
+  const ModParams m = mods[limb];
+  u64 hm[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) hm[k] = hat[(u64)k * hs + limb].y;
+  const u32 tp = Lay0::tpos(t);
+  const gptr_u64 yb = (gptr_u64)(y + (u64)b * S * N + (u64)tile * G::SUBS_C + sub);
+  u64 x[kE];
+#pragma unroll
+  for (int j = 0; j < kE; ++j) {
+    const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
+    u128 acc = 0;
+#pragma unroll
+    for (int k = 0; k < S; ++k) acc += (u128)yb[(u64)k * N + i] * hm[k];
+    x[j] = csub(mont_reduce_lazy((u64)acc, (u64)(acc >> 64), m.q, m.qinv), m.q);
+  }
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, false, H, 1>(
+      x, GView<G::R2>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
+      tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
+}
+
 // Fused key-switch row kernel: the row-forward NTT of every ModUp digit plus the inner product
 // with the evaluation key, so the extended digits never go back to HBM in NTT form and no separate
 // inner-product pass re-reads them (SURVEY §8a' key-switch; the unfused path is k_ntt_row per digit
@@ -1261,6 +1321,42 @@ int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst,
       col_fwd_pass<n, 8>(c, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);         \
     FHE_HIP_CHECK(hipGetLastError());                                                       \
     return kOk;
+    FHE_LOGN_CASES(X)
+#undef X
+  }
+  set_error("unsupported log_n");
+  return kUnsupported;
+}
+
+namespace {
+template <int LOGN, int HD>
+int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
+  using G = Geo<LOGN>;
+  const dim3 g((u32)((u64)a.T * a.batch * G::TILES_C));
+  switch (a.S) {
+#define D(k)                                                                                     \
+  case k:                                                                                        \
+    k_modup_col<LOGN, HD, k><<<g, G::THR_C, 0, s>>>(a.y, a.ext, a.rn, a.T, a.skip_at,            \
+                                                    a.skip_len, a.n0, a.base0, a.base1, a.batch, \
+                                                    a.hat, a.hs, c->d_tw_fwd, c->d_mods);        \
+    break;
+    D(1) D(2) D(3) D(4) D(5) D(6) D(7)
+#undef D
+    default:
+      set_error("modup_col: digits of more than 7 limbs take the unfused path");
+      return kUnsupported;
+  }
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+}  // namespace
+
+int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
+  if ((u64)a.T * a.batch == 0) return kOk;
+  switch (c->log_n) {
+#define X(n) \
+  case n:    \
+    return c->lz16 ? modup_col_dispatch<n, 16>(c, a, s) : modup_col_dispatch<n, 8>(c, a, s);
     FHE_LOGN_CASES(X)
 #undef X
   }

@@ -22,6 +22,9 @@ constexpr int kMaxSrc = 16;
 #ifndef FHE_KS_FUSED
 #define FHE_KS_FUSED 1
 #endif
+#ifndef FHE_MODUP_FUSED
+#define FHE_MODUP_FUSED 1
+#endif
 
 // out row r -> ctx limb: r < n0 ? base0 + r : base1 + (r - n0)
 struct RowMap {
@@ -158,6 +161,22 @@ __global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ o
   out1[e] = csub(shoup_lazy(acc[acc_ws + ai] + q - c1, w.x, w.y, q), q);
 }
 
+// ModUp prologue for the fused column pass (ntt.hip k_modup_col): y[b][k][i] = [x_k (D^_k)^-1]_{d_k}
+// over the digit's S source rows of c_all [batch][L][N].  Grid: x over coefficients, y = k, z = b.
+__global__ __launch_bounds__(kThreads) void k_modup_scale(const u64* __restrict__ c_all, u64 in_bs,
+                                                          u32 src0, u64* __restrict__ y, u32 S,
+                                                          u32 log_n,
+                                                          const ulonglong2* __restrict__ inv,
+                                                          const ModParams* __restrict__ mods) {
+  const u64 n = 1ull << log_n;
+  const u32 k = blockIdx.y, b = blockIdx.z;
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u64 q = mods[src0 + k].q;
+  const ulonglong2 w = inv[k];
+  y[((u64)b * S + k) * n + i] =
+      csub(shoup_lazy(c_all[(u64)b * in_bs + (u64)(src0 + k) * n + i], w.x, w.y, q), q);
+}
+
 template <class T>
 int upload(T** dptr, const std::vector<T>& v) {
   if (v.empty()) return kOk;
@@ -281,8 +300,9 @@ int build_rns_tables(fhe_ctx* c) {
 size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch) {
   const u64 rows = nlimbs + c->K;
   // ext [dnum][batch][rows][N] + acc [2][batch][rows][N] + conv [2][batch][nlimbs][N]
-  // + c_all [batch][L][N] (single-device form)
-  return (u64)batch * ((u64)c->dnum * rows + 2 * rows + 2 * nlimbs + c->L) * c->n * sizeof(u64);
+  // + y [batch][alpha][N] (fused ModUp) + c_all [batch][L][N] (single-device form, at the tail)
+  return (u64)batch * ((u64)c->dnum * rows + 2 * rows + 2 * nlimbs + c->alpha + c->L) * c->n *
+         sizeof(u64);
 }
 
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_all,
@@ -309,6 +329,11 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   // kernel (ntt.hip, k_ks_row_inner) runs every digit's row-forward pass and the inner product
   // (no NTT-form ext in HBM, no separate inner-product pass); otherwise full NTTs + k_ks_inner.
   const bool fused = FHE_KS_FUSED && c->dnum <= 4;
+  // FHE_MODUP_FUSED (with the fused row kernel, digits of <= 7 limbs): the base conversion runs
+  // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
+  // digit's source rows; the extended rows are never written in coefficient form.
+  const bool fused_up = fused && FHE_MODUP_FUSED && alpha <= 7;
+  u64* yws = conv + 2 * B * (u64)nlimbs * n;  // [B][alpha][N]
   auto ntt_fwd = [&](u64* p, u32 l0, u32 nl) {
     return fused ? launch_ntt_col_fwd(c, p, rn, p, rn, batch, l0, nl, s)
                  : launch_ntt(c, true, p, p, batch, rn, l0, nl, s);
@@ -317,6 +342,20 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   for (u32 j = 0; j < c->dnum; ++j) {
     const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
     u64* e = ext + (u64)j * B * rn;
+    if (fused_up) {
+      const u32 S = hi - lo;
+      k_modup_scale<<<dim3((u32)(n / kThreads), S, batch), kThreads, 0, s>>>(
+          c_all, (u64)L * n, lo, yws, S, c->log_n, c->d_modup_inv + (size_t)j * alpha, c->d_mods);
+      FHE_HIP_CHECK(hipGetLastError());
+      // this rank's own rows of digit j are skipped: ks_row_inner takes them from d2_own
+      const u32 own_lo = std::max(lo, limb0), own_hi = std::min(hi, limb0 + nlimbs);
+      const u32 skip_len = own_hi > own_lo ? own_hi - own_lo : 0;
+      const u32 skip_at = skip_len ? own_lo - limb0 : rows;
+      const ModUpColArgs ma{yws, e, rn, S, rows - skip_len, skip_at, skip_len, nlimbs, limb0, L,
+                            batch, c->d_modup_hat + (size_t)j * alpha * M, M};
+      if ((rc = launch_modup_col(c, ma, s))) return rc;
+      continue;
+    }
     const BcArgs up{c_all + (u64)lo * n, (u64)L * n, lo, e, rn, rows, map, lo, hi, batch};
     if ((rc = baseconv_any(hi - lo, up, n, c->d_modup_inv + (size_t)j * alpha,
                            c->d_modup_hat + (size_t)j * alpha * M, M, c->d_mods, s)))
