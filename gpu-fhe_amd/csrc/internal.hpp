@@ -109,6 +109,17 @@ struct ModUpColArgs {
   u32 hs;
 };
 int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s);
+// ModDown finish fused into the conversion NTT's row-forward pass (ntt.hip, k_moddown_row): conv
+// [2][batch][nq][N] column-passed -> ks{0,1} [batch][nq][N] = (acc - NTT(conv)) P^-1 mod q.
+struct ModDownRowArgs {
+  const u64* conv;
+  u64* ks0;
+  u64* ks1;
+  const u64* acc;
+  u64 acc_ws;
+  u32 rows, nq, limb0, batch;
+};
+int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s);
 // Fused ct x ct tensor: a, b [batch][2][nlimbs][N] coefficient form -> d [batch][3][nlimbs][N].
 int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                    u32 nlimbs, void* ws, hipStream_t s);

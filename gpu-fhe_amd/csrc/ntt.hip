@@ -1006,6 +1006,67 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
 }
 
+// ModDown's last step fused into the row-forward pass of the conversion NTT (key-switch):
+// conv [2][batch][nq][N] arrives column-passed; each row finishes its forward NTT in registers
+// and, instead of storing NTT(conv), stores out_h = (acc_h - NTT(conv_h)) P^-1 mod q straight into
+// ks0 / ks1 [batch][nq][N] (acc_h [batch][rows][N], its own Q-limb rows first).  Saves the
+// NTT-form conv round trip and the separate finish pass (rns.hip k_moddown_finish).
+struct FinishView {
+  u64* out;
+  const u64* acc;
+  u32 lane;
+  u64 q;
+  ulonglong2 pinv;
+  template <class Lay>
+  __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
+    static_assert(contiguous16<Lay>(), "the last forward row round is contiguous");
+    const u32 off = lane + tp;
+    const gptr_u128 a = (gptr_u128)(acc + off);
+    const gptr_u128 o = (gptr_u128)(out + off);
+#pragma unroll
+    for (int j = 0; j < kE / 2; ++j) {
+      const u64x2_t av = a[j];
+      const u64 r0 = csub(shoup_lazy(av.x + q - x[2 * j], pinv.x, pinv.y, q), q);
+      const u64 r1 = csub(shoup_lazy(av.y + q - x[2 * j + 1], pinv.x, pinv.y, q), q);
+      o[j] = u64x2_t{r0, r1};
+    }
+  }
+};
+
+template <int LOGN, int H>
+__global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __restrict__ ks0,
+                                        u64* __restrict__ ks1, const u64* __restrict__ acc,
+                                        u64 acc_ws, u32 rows, u32 nq, u32 limb0, u32 batch,
+                                        u32 items, const ulonglong2* __restrict__ pinv,
+                                        const ulonglong2* __restrict__ tw_all,
+                                        const ModParams* __restrict__ mods) {
+  using G = Geo<LOGN>;
+  constexpr u64 N = 1ull << LOGN;
+  __shared__ u64 lds[G::LDS_R];
+  const u32 t = threadIdx.x % G::TPS_R, sub = threadIdx.x / G::TPS_R;
+  const LView<1, true> lv{lds + sub * G::RS};
+  const u32 it = blockIdx.x;
+  if (it >= items) return;
+  const u32 polys = 2 * batch;
+  u32 l, rest;
+  xcd_limb_split(it, nq, items / nq, l, rest);
+  const u32 p = rest % polys, tile = rest / polys;
+  const u32 h = p / batch, b = p % batch;
+  const u32 row0 = tile * G::SUBS_R;
+  const u32 limb = __builtin_amdgcn_readfirstlane(limb0 + l);
+  const u64 q = mods[limb].q;
+  const u32 lane = sub * G::R2;
+  const u64 rloc = (u64)row0 * G::R2;
+  u64 x[kE];
+  pass_load<G::N2, true>(GView<1>{const_cast<u64*>(conv) + ((u64)p * nq + l) * N + rloc, lane}, t,
+                         x);
+  const FinishView fo{(h ? ks1 : ks0) + ((u64)b * nq + l) * N + rloc,
+                      acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc, lane, q,
+                      pinv[limb]};
+  pass_run<G::N2, true, kFinalFwd, kWaveSync, true, false, H, fwd_range(1, G::N1, H)>(
+      x, fo, lv, t, tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, q, {0, 0}, {0, 0});
+}
+
 // Fused key-switch row kernel: the row-forward NTT of every ModUp digit plus the inner product
 // with the evaluation key, so the extended digits never go back to HBM in NTT form and no separate
 // inner-product pass re-reads them (SURVEY §8a' key-switch; the unfused path is k_ntt_row per digit
@@ -1357,6 +1418,35 @@ int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
 #define X(n) \
   case n:    \
     return c->lz16 ? modup_col_dispatch<n, 16>(c, a, s) : modup_col_dispatch<n, 8>(c, a, s);
+    FHE_LOGN_CASES(X)
+#undef X
+  }
+  set_error("unsupported log_n");
+  return kUnsupported;
+}
+
+namespace {
+template <int LOGN, int HD>
+void moddown_row_dispatch(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s) {
+  using G = Geo<LOGN>;
+  const u64 items = (u64)2 * a.batch * a.nq * G::TILES_R;
+  k_moddown_row<LOGN, HD><<<dim3((u32)((items + 7) / 8 * 8)), G::THR_R, 0, s>>>(
+      a.conv, a.ks0, a.ks1, a.acc, a.acc_ws, a.rows, a.nq, a.limb0, a.batch, (u32)items,
+      c->d_pinv, c->d_tw_fwd, c->d_mods);
+}
+}  // namespace
+
+int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s) {
+  if ((u64)a.batch * a.nq == 0) return kOk;
+  switch (c->log_n) {
+#define X(n)                                                                                   \
+  case n:                                                                                      \
+    if (c->lz16)                                                                               \
+      moddown_row_dispatch<n, 16>(c, a, s);                                                    \
+    else                                                                                       \
+      moddown_row_dispatch<n, 8>(c, a, s);                                                     \
+    FHE_HIP_CHECK(hipGetLastError());                                                         \
+    return kOk;
     FHE_LOGN_CASES(X)
 #undef X
   }

@@ -393,6 +393,16 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   if ((rc = baseconv_any(K, down, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, s)))
     return rc;
   prof_mark(s, "ks_moddown_conv");
+  if (fused) {  // conversion NTT's row pass finishes ModDown in its epilogue
+    if ((rc = launch_ntt_col_fwd(c, conv, (u64)nlimbs * n, conv, (u64)nlimbs * n, 2 * batch, limb0,
+                                 nlimbs, s)))
+      return rc;
+    prof_mark(s, "ks_moddown_col");
+    const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch};
+    if ((rc = launch_moddown_row(c, da, s))) return rc;
+    prof_mark(s, "moddown_row_finish");
+    return kOk;
+  }
   if ((rc = launch_ntt(c, true, conv, conv, 2 * batch, (u64)nlimbs * n, limb0, nlimbs, s)))
     return rc;
   k_moddown_finish<<<dim3((u32)(n / kThreads), nlimbs, batch), kThreads, 0, s>>>(
