@@ -1239,7 +1239,7 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
                                                c->d_mods);
 }
 
-#if !FHE_NTT_ROW_ONLY
+#if !FHE_NTT_ROW_ONLY && !FHE_NTT_KS_ONLY
 // FHE_ROW_E8: the standalone row passes come from ntt_row_e8.hip, this file rebuilt with E = 8
 // elements per thread (half the VGPRs and LDS per wave: twice the resident waves to hide the row
 // twiddles' L2 latency; measured row-forward -9 %, row-inverse -2 %).  The fused HomMult kernel
@@ -1334,7 +1334,7 @@ int launch_ntt_row_e8(const fhe_ctx* c, bool forward, const u64* src, u64 spstri
   set_error("unsupported log_n");
   return kUnsupported;
 }
-#else
+#elif FHE_NTT_KS_ONLY
 
 namespace {
 template <int LOGN, int HD>
@@ -1401,10 +1401,10 @@ int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
                                                     a.skip_len, a.n0, a.base0, a.base1, a.batch, \
                                                     a.hat, a.hs, c->d_tw_fwd, c->d_mods);        \
     break;
-    D(1) D(2) D(3) D(4) D(5) D(6) D(7)
+    D(1) D(2) D(3) D(4)
 #undef D
     default:
-      set_error("modup_col: digits of more than 7 limbs take the unfused path");
+      set_error("modup_col: digits of more than 4 limbs take the unfused path");
       return kUnsupported;
   }
   FHE_HIP_CHECK(hipGetLastError());
@@ -1466,6 +1466,8 @@ int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
   set_error("unsupported log_n");
   return kUnsupported;
 }
+
+#else
 
 int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 polys, u64 pstride,
                u32 limb0, u32 nlimbs, hipStream_t s) {
@@ -1540,6 +1542,6 @@ int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 bat
   return kOk;
 }
 
-#endif  // FHE_NTT_ROW_ONLY
+#endif  // FHE_NTT_ROW_ONLY / FHE_NTT_KS_ONLY
 
 }  // namespace fhe

@@ -329,10 +329,10 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   // kernel (ntt.hip, k_ks_row_inner) runs every digit's row-forward pass and the inner product
   // (no NTT-form ext in HBM, no separate inner-product pass); otherwise full NTTs + k_ks_inner.
   const bool fused = FHE_KS_FUSED && c->dnum <= 4;
-  // FHE_MODUP_FUSED (with the fused row kernel, digits of <= 7 limbs): the base conversion runs
+  // FHE_MODUP_FUSED (with the fused row kernel, digits of <= 4 limbs): the base conversion runs
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
   // digit's source rows; the extended rows are never written in coefficient form.
-  const bool fused_up = fused && FHE_MODUP_FUSED && alpha <= 7;
+  const bool fused_up = fused && FHE_MODUP_FUSED && alpha <= 4;
   u64* yws = conv + 2 * B * (u64)nlimbs * n;  // [B][alpha][N]
   auto ntt_fwd = [&](u64* p, u32 l0, u32 nl) {
     return fused ? launch_ntt_col_fwd(c, p, rn, p, rn, batch, l0, nl, s)
