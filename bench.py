@@ -49,7 +49,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch", "mulrelin", "ntt-batch"],
                     default="hommult")
-    ap.add_argument("--batch", type=int, default=16, help="ciphertexts per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="ciphertexts per GPU per step (default 64 for hommult -- the throughput "
+                         "batch: +3.5 %% over 16, fewer launch tails -- and 16 for the others)")
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -388,6 +390,8 @@ def run_mulrelin(args, world, rank):
 
 def main():
     args = parse()
+    if args.batch is None:
+        args.batch = 64 if args.workload == "hommult" else 16
     world, rank = dist_setup(args)
     run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch,
            "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch}[args.workload]
