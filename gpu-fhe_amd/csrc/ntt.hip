@@ -683,7 +683,11 @@ struct Geo {
 // TILED: dst limb rows are written tile-major -- column tile k (SUBS_C columns x R1 rows) as one
 // contiguous block [k][row][SUBS_C] -- so every workgroup's output is one contiguous run of
 // R1 SUBS_C words (the HomMult workspace; the fused row kernel reads it through TView).
-template <int LOGN, bool FWD, int H = 8, bool TILED = false>
+// CFIN (forward only): the column pass's final reduction, kNotFinal (values below
+// fwd_range(1, N1, H) q) or kFinalFwd2 (below 2q: HomMult, whose fused row kernel then starts its
+// lazy ranges at 2q and saves two reduction stages -- VALU moved from the VALU-bound fused kernel
+// into the memory-bound column pass).
+template <int LOGN, bool FWD, int H = 8, bool TILED = false, int CFIN = kNotFinal>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_ntt_col(const u64* __restrict__ src,
                                                       const u64* __restrict__ src2,
@@ -728,7 +732,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       nf1 = nfold[4 * cur.limb + 1];
     }
     using GOut = GView<TILED ? G::SUBS_C : G::R2>;
-    pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
+    pass_run<G::N1, FWD, FWD ? CFIN : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
         x, GOut{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
         nf0, nf1, prefetch);
     if (!more) break;
@@ -821,7 +825,16 @@ struct HmGeo {
   static constexpr int SYNC_ROUND = (POLY_MAJOR || LANES_ROW <= 64) ? kWaveSync : kBlockSync;
 };
 
-template <int LOGN, int HR = 8, bool TILED = false>
+// FHE_HM_COL_REDUCE: HomMult's column-forward pass leaves its output below 2q (CFIN kFinalFwd2)
+// and the fused kernel's forward ranges start there (kHmColOut); else the column pass's lazy
+// range (11q at 16q headroom) carries into the fused kernel.  Measured: column-forward +11 %
+// (114 -> 126 us: it is not VALU-idle enough to absorb 3 subtractions per element), fused kernel
+// unchanged within noise.  Off; kept as an A/B switch.
+#ifndef FHE_HM_COL_REDUCE
+#define FHE_HM_COL_REDUCE 0
+#endif
+template <int LOGN, int HR = 8, bool TILED = false,
+          int kHmColOut = FHE_HM_COL_REDUCE ? 2 : fwd_range(1, Geo<LOGN>::N1, HR)>
 __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
                                                           u64* __restrict__ d, u32 nlimbs,
                                                           u32 limb0,
@@ -870,7 +883,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
     constexpr int KB = Rd::kb(k);
     constexpr int LO = Rd::lo_fwd(k);
     constexpr int F = (k == Rd::NR - 1) ? kFinalFwd2 : kNotFinal;
-    constexpr int RIN = fwd_range(fwd_range(1, G::N1, HR), G::N2 - (LO + KB), HR);
+    constexpr int RIN = fwd_range(kHmColOut, G::N2 - (LO + KB), HR);
     using Lay = Layout<G::N2, KB, LO>;
     const u32 tp = Lay::tpos(t);
     if constexpr (k == 0) {
@@ -1294,7 +1307,8 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   const PolyMap to_x{4, 2 * limbN, limbN, 4 * limbN, limbN, 2};
   const u64 ic = (u64)batch * 4 * nlimbs * G::TILES_C;
   constexpr bool TL = FHE_HM_TILED != 0;
-  k_ntt_col<LOGN, true, HD, TL><<<item_grid<k_ntt_col<LOGN, true, HD, TL>, kLoopCol>(c, G::THR_C, ic),
+  constexpr int CF = FHE_HM_COL_REDUCE ? kFinalFwd2 : kNotFinal;
+  k_ntt_col<LOGN, true, HD, TL, CF><<<item_grid<k_ntt_col<LOGN, true, HD, TL, CF>, kLoopCol>(c, G::THR_C, ic),
                                   G::THR_C, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic,
                                                     c->d_tw_fwd, c->d_nfold, c->d_mods);
   prof_mark(s, "hm_col_fwd");
