@@ -274,7 +274,11 @@ __device__ __forceinline__ ulonglong2 ld_tw(const ulonglong2* p) {
 #endif
 __device__ __forceinline__ u64 csubk(u64 x, u64 m) {
 #if FHE_CSUB_FAST
-  return csub_fast(x, 0 - m);
+  // -m as an opaque uniform: otherwise x + (0 - m) folds back into a borrow chain (sub_co/subb,
+  // two instructions) instead of one v_lshl_add_u64
+  u64 nm = 0 - m;
+  asm("" : "+s"(nm));
+  return csub_fast(x, nm);
 #else
   return csub(x, m);
 #endif
