@@ -1,0 +1,93 @@
+"""Edge cases of the HIP path (GPU): empty batches, ragged reference-shim shapes, the largest limb
+count and transform size, all-maximum residues, and the bench's own HomMult shape checked
+bit-exact against the C oracle.  Everything goes through the C ABI (ctypes); the oracle is only
+the checker."""
+import numpy as np
+import pytest
+
+import coracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fc():
+    import fhecore
+
+    return fhecore
+
+
+def rand(mods, log_n, lead=(), seed=0):
+    rng = np.random.default_rng(seed)
+    n = 1 << log_n
+    return np.stack([rng.integers(0, q, size=lead + (n,), dtype=np.uint64) for q in mods],
+                    axis=len(lead))
+
+
+def test_empty_batches_are_noops(fc):
+    """Zero polynomials / ciphertexts: every entry point returns at once, shapes preserved."""
+    import torch
+
+    ctx = fc.Context(12, L=2)
+    n = 1 << 12
+    t = torch.empty(0, 2, n, dtype=torch.int64, device="cuda")
+    ctx.ntt_(t)
+    ctx.intt_(t)
+    assert tuple(t.shape) == (0, 2, n)
+    assert tuple(ctx.vec("add", t, t).shape) == (0, 2, n)
+    a = torch.empty(0, 2, 2, n, dtype=torch.int64, device="cuda")
+    d = ctx.hommult(a, a)
+    assert tuple(d.shape) == (0, 3, 2, n)
+
+
+@pytest.mark.parametrize("shape", [(7,), (3, 5), (2, 3, 5), (1, 1), (0,), (4, 0)])
+@pytest.mark.parametrize("op", ["vec_add", "vec_sub", "vec_mul"])
+def test_reference_shim_ragged_shapes(fc, shape, op):
+    """arithmetic.vec_* on shapes no kernel tiles evenly (odd lengths, empty axes), exact values
+    (the reference's semantics on object-dtype input, /root/reference/arithmetic.py:3-13)."""
+    import arithmetic
+
+    q = (1 << 60) - 93  # any modulus: the generic vec_op_mod path
+    rng = np.random.default_rng(len(shape) * 10 + sum(shape))
+    a = rng.integers(0, q, size=shape, dtype=np.uint64)
+    b = rng.integers(0, q, size=shape, dtype=np.uint64)
+    got = np.asarray(getattr(arithmetic, op)(a, b, q))
+    f = {"vec_add": lambda x, y: (x + y) % q, "vec_sub": lambda x, y: (x - y) % q,
+         "vec_mul": lambda x, y: (x * y) % q}[op]
+    want = np.array([f(int(x), int(y)) for x, y in zip(a.reshape(-1), b.reshape(-1))],
+                    dtype=object).reshape(shape)
+    assert got.shape == shape
+    assert all(int(x) == int(y) for x, y in zip(got.reshape(-1), want.reshape(-1)))
+
+
+def test_ntt_many_limbs_round_trip(fc):
+    """64 RNS limbs (the most a context takes) at N = 2^11: forward vs oracle, inverse back."""
+    ctx = fc.Context(11, L=64)
+    x = rand(ctx.moduli, 11, (1,), seed=64)
+    t = fc.to_device(x)
+    ctx.ntt_(t)
+    assert (fc.to_host(t) == coracle.ntt_fwd(x, ctx.moduli)).all()
+    ctx.intt_(t)
+    assert (fc.to_host(t) == x).all()
+
+
+def test_ntt_all_max_residues_largest_n(fc):
+    """q - 1 in every coefficient at N = 2^17 (the deepest lazy ranges), 2 limbs."""
+    ctx = fc.Context(17, L=2)
+    n = 1 << 17
+    x = np.stack([np.full(n, q - 1, dtype=np.uint64) for q in ctx.moduli])[None]
+    t = fc.to_device(x)
+    ctx.ntt_(t)
+    assert (fc.to_host(t) == coracle.ntt_fwd(x, ctx.moduli)).all()
+    ctx.intt_(t)
+    assert (fc.to_host(t) == x).all()
+
+
+def test_hommult_bench_shape_matches_oracle(fc):
+    """bench.py's default HomMult shape (N = 2^16, 8 limbs, 64 ciphertext pairs per GPU), every
+    output word compared with the C oracle."""
+    ctx = fc.Context(16, L=8)
+    a = rand(ctx.moduli, 16, (64, 2), seed=640)
+    b = rand(ctx.moduli, 16, (64, 2), seed=641)
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    assert (d == coracle.hommult(a, b, ctx.moduli)).all()
