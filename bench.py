@@ -323,6 +323,7 @@ def run_keyswitch(args, world, rank):
 
     class Eng:  # the Context, with a preallocated workspace
         intt_ = ctx.intt_
+        intt = ctx.intt
 
         @staticmethod
         def keyswitch_shard(c_all, d2_own, eb, ea, limb0):

@@ -185,6 +185,20 @@ int fhe_ntt_inv(const fhe_ctx* c, uint64_t* data, uint32_t polys, uint32_t limb0
   return launch_ntt(c, false, data, data, polys, (uint64_t)nlimbs * c->n, limb0, nlimbs, hs(s));
 }
 
+int fhe_ntt_fwd_to(const fhe_ctx* c, uint64_t* dst, const uint64_t* src, uint32_t polys,
+                   uint32_t limb0, uint32_t nlimbs, fhe_stream_t s) {
+  int rc = check_window(c, limb0, nlimbs, c ? c->L + c->K : 0, "fhe_ntt_fwd_to");
+  if (rc) return rc;
+  return launch_ntt(c, true, src, dst, polys, (uint64_t)nlimbs * c->n, limb0, nlimbs, hs(s));
+}
+
+int fhe_ntt_inv_to(const fhe_ctx* c, uint64_t* dst, const uint64_t* src, uint32_t polys,
+                   uint32_t limb0, uint32_t nlimbs, fhe_stream_t s) {
+  int rc = check_window(c, limb0, nlimbs, c ? c->L + c->K : 0, "fhe_ntt_inv_to");
+  if (rc) return rc;
+  return launch_ntt(c, false, src, dst, polys, (uint64_t)nlimbs * c->n, limb0, nlimbs, hs(s));
+}
+
 size_t fhe_hommult_workspace(const fhe_ctx* c, uint32_t batch, uint32_t nlimbs) {
   return c ? hommult_workspace_bytes(c, batch, nlimbs) : 0;
 }
@@ -228,11 +242,10 @@ int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t
   if (rc) return rc;
   const size_t bytes = keyswitch_workspace_bytes(c, c->L, batch);
   if ((rc = ensure_ws(c, bytes, &ws))) return rc;
-  // c_all = INTT(d2) lives at the tail of the workspace
+  // c_all = INTT(d2) lives at the tail of the workspace (out of place: no copy of d2)
   const size_t call = (size_t)batch * c->L * c->n * sizeof(uint64_t);
   uint64_t* c_all = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + bytes - call);
-  FHE_HIP_CHECK(hipMemcpyAsync(c_all, d2, call, hipMemcpyDeviceToDevice, hs(s)));
-  if ((rc = launch_ntt(c, false, c_all, c_all, batch, (uint64_t)c->L * c->n, 0, c->L, hs(s))))
+  if ((rc = launch_ntt(c, false, d2, c_all, batch, (uint64_t)c->L * c->n, 0, c->L, hs(s))))
     return rc;
   return launch_keyswitch_shard(c, ks0, ks1, c_all, d2, evk_b, evk_a, 0, c->L, batch, ws, hs(s));
 }

@@ -38,6 +38,8 @@ SIGNATURES = {
     "fhe_vec_op_mod": (_i32, [_i32, _vp, _vp, _vp, _u64, _u64, _u64p, _u64, _i32, _i32, _vp]),
     "fhe_ntt_fwd": (_i32, [_vp, _vp, _u32, _u32, _u32, _vp]),
     "fhe_ntt_inv": (_i32, [_vp, _vp, _u32, _u32, _u32, _vp]),
+    "fhe_ntt_fwd_to": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _vp]),
+    "fhe_ntt_inv_to": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _vp]),
     "fhe_hommult_workspace": (_sz, [_vp, _u32, _u32]),
     "fhe_hommult": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
     "fhe_baseconv": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _vp]),

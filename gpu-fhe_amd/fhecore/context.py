@@ -161,6 +161,27 @@ class Context:
     def intt_(self, t, limb0: int = 0):
         return self._ntt(t, limb0, False)
 
+    def ntt(self, t, out=None, limb0: int = 0):
+        """Out-of-place forward NTT: returns out = NTT(t) (a new tensor unless `out` is given);
+        t is left untouched and nothing is copied (the first pass reads t, writes out)."""
+        return self._ntt_to(t, out, limb0, True)
+
+    def intt(self, t, out=None, limb0: int = 0):
+        return self._ntt_to(t, out, limb0, False)
+
+    def _ntt_to(self, t, out, limb0, fwd):
+        _check_tensor(t, "ntt", (self.n,))
+        if out is None:
+            out = torch.empty_like(t)
+        elif out.shape != t.shape or out.dtype != t.dtype or not out.is_contiguous():
+            raise _capi.FheError("ntt: out must be a contiguous tensor shaped like the input")
+        nl = t.shape[-2] if t.dim() >= 2 else 1
+        polys = t.numel() // (nl * self.n)
+        fn = load().fhe_ntt_fwd_to if fwd else load().fhe_ntt_inv_to
+        with torch.cuda.device(self.device):
+            check(fn(self._ptr, _ptr(out), _ptr(t), polys, limb0, nl, _stream(t)), fn.__name__)
+        return out
+
     def _ntt(self, t, limb0, fwd):
         _check_tensor(t, "ntt", (self.n,))
         nl = t.shape[-2] if t.dim() >= 2 else 1

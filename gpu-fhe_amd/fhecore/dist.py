@@ -9,8 +9,9 @@ the K special limbs (so ModDown needs no second collective).  Outputs stay limb-
 concatenate to the single-device result bit for bit.
 
 The orchestration is written against an "engine" with two methods -- ``intt_(t, limb0)`` and
-``keyswitch_shard(c_all, d2_own, evk_b, evk_a, limb0)`` -- so fhecore.Context (the HIP path) and a
-CPU restatement used by the gloo tests run the same code.
+``keyswitch_shard(c_all, d2_own, evk_b, evk_a, limb0)``, plus an optional out-of-place
+``intt(t, limb0)`` that saves the copy of d2 -- so fhecore.Context (the HIP path) and a CPU
+restatement used by the gloo tests run the same code.
 """
 from __future__ import annotations
 
@@ -90,7 +91,10 @@ def sharded_keyswitch(engine, d2_own, evk_b_own, evk_a_own, shard: LimbShard, gr
     d2_own: [..., nlimbs, N] NTT form (limbs [lo, hi), any leading batch shape); evk_*_own:
     [dnum, nlimbs + K, N] (own Q-limbs then the K P-limbs, see LimbShard.evk_rows), one key for the
     batch.  Returns (ks0_own, ks1_own) shaped like d2_own, NTT form."""
-    c_own = d2_own.clone()
-    engine.intt_(c_own, limb0=shard.lo)
+    if hasattr(engine, "intt"):  # out of place: no copy of d2 (the HIP Context)
+        c_own = engine.intt(d2_own, limb0=shard.lo)
+    else:
+        c_own = d2_own.clone()
+        engine.intt_(c_own, limb0=shard.lo)
     c_all = all_gather_limbs(c_own, shard, group)  # the only collective of the whole path
     return engine.keyswitch_shard(c_all, d2_own, evk_b_own, evk_a_own, shard.lo)

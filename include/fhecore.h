@@ -100,6 +100,13 @@ int fhe_ntt_fwd(const fhe_ctx* ctx, uint64_t* data, uint32_t polys, uint32_t lim
                 uint32_t nlimbs, fhe_stream_t stream);
 int fhe_ntt_inv(const fhe_ctx* ctx, uint64_t* data, uint32_t polys, uint32_t limb0,
                 uint32_t nlimbs, fhe_stream_t stream);
+/* Out of place: dst = NTT(src) / INTT(src), both [polys][nlimbs][N]; src is left untouched (the
+ * first pass reads src and writes dst, the second runs in place on dst -- no copy).  dst == src is
+ * the in-place call; other overlaps are undefined. */
+int fhe_ntt_fwd_to(const fhe_ctx* ctx, uint64_t* dst, const uint64_t* src, uint32_t polys,
+                   uint32_t limb0, uint32_t nlimbs, fhe_stream_t stream);
+int fhe_ntt_inv_to(const fhe_ctx* ctx, uint64_t* dst, const uint64_t* src, uint32_t polys,
+                   uint32_t limb0, uint32_t nlimbs, fhe_stream_t stream);
 
 /* ---- ct x ct homomorphic multiplication (tensor) ----------------------------------------
  * a, b: [batch][2][nlimbs][N] coefficient form; d: [batch][3][nlimbs][N] coefficient form with

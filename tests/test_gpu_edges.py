@@ -91,3 +91,16 @@ def test_hommult_bench_shape_matches_oracle(fc):
     b = rand(ctx.moduli, 16, (64, 2), seed=641)
     d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
     assert (d == coracle.hommult(a, b, ctx.moduli)).all()
+
+
+@pytest.mark.parametrize("log_n,L", [(12, 3), (16, 8)])
+def test_out_of_place_ntt_leaves_source(fc, log_n, L):
+    """fhe_ntt_fwd_to / fhe_ntt_inv_to (Context.ntt / intt): dst = NTT(src), src untouched."""
+    ctx = fc.Context(log_n, L=L)
+    x = rand(ctx.moduli, log_n, (2,), seed=log_n + L)
+    src = fc.to_device(x)
+    y = ctx.ntt(src)
+    assert (fc.to_host(src) == x).all()
+    assert (fc.to_host(y) == coracle.ntt_fwd(x, ctx.moduli)).all()
+    z = ctx.intt(y)
+    assert (fc.to_host(z) == x).all() and (fc.to_host(y) == coracle.ntt_fwd(x, ctx.moduli)).all()
