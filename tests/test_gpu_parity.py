@@ -240,6 +240,27 @@ def test_keyswitch_matches_oracle(fc, L, K, dnum):
     assert (fc.to_host(ks0) == r0).all() and (fc.to_host(ks1) == r1).all()
 
 
+@pytest.mark.parametrize("L,K,dnum,batch", [
+    (10, 2, 2, 2),   # digits of 5 limbs: fused row kernel, unfused ModUp (k_baseconv + column pass)
+    (12, 3, 6, 1),   # dnum 6 > 4: the fully unfused path (full NTTs + k_ks_inner + k_moddown_finish)
+    (16, 4, 4, 3),   # batched, the fused path end to end
+    (7, 2, 3, 2),    # a ragged last digit (7 = 3 + 3 + 1)
+])
+def test_keyswitch_paths_match_oracle(fc, L, K, dnum, batch):
+    """Every key-switch code path (fused / partly fused / unfused, ragged digits, batches) against
+    the C oracle at N = 2^12."""
+    ctx = ctx_for(fc, 12, L, K=K, dnum=dnum)
+    allm = ctx.all_moduli
+    d2 = rand(ctx.moduli, 12, (batch,), seed=70 + L)
+    eb = rand(allm, 12, (dnum,), seed=71)
+    ea = rand(allm, 12, (dnum,), seed=72)
+    ks0, ks1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(eb), fc.to_device(ea))
+    h0, h1 = fc.to_host(ks0), fc.to_host(ks1)
+    for b in range(batch):
+        r0, r1 = coracle.keyswitch(d2[b], eb, ea, ctx.moduli, ctx.special, dnum)
+        assert (h0[b] == r0).all() and (h1[b] == r1).all(), b
+
+
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_keyswitch_sharded_equals_unsharded(fc, G):
     """the G-way limb-sharded key-switch (one all-gather of INTT(d2)) concatenates to
