@@ -494,7 +494,24 @@ constexpr bool contiguous16() {
 // lgkmcnt and so make every LDS wait wait for them.)
 using gptr_u64 = __attribute__((address_space(1))) u64*;
 using gptr_u128 = __attribute__((address_space(1))) u64x2_t*;
-template <int STRIDE>
+// NT views: non-temporal loads / stores for data streamed once through a working set larger
+// than the caches.  HomMult's fused row kernel and its column-inverse pass use them (measured
+// +1.5-2 % HomMult/s at batch 16-64: column inverse -6 %, fused kernel -2 %); the standalone NTT
+// does not (its second pass re-reads what the first wrote, and the Infinity Cache serves part of
+// it: non-temporal there costs 20 %).
+template <bool NT, class P>
+__device__ __forceinline__ auto gld(P p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, class P, class V>
+__device__ __forceinline__ void gst(P p, V v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+template <int STRIDE, bool NT = false>
 struct GView {
   u64* base;
   u32 lane;
@@ -505,13 +522,13 @@ struct GView {
       const gptr_u128 v = (gptr_u128)(base + off);
 #pragma unroll
       for (int j = 0; j < kE / 2; ++j) {
-        const u64x2_t w = v[j];
+        const u64x2_t w = gld<NT>(v + j);
         x[2 * j] = w.x;
         x[2 * j + 1] = w.y;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) x[j] = ((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE))[off];
+      for (int j = 0; j < kE; ++j) x[j] = gld<NT>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off);
     }
   }
   template <class Lay>
@@ -520,10 +537,10 @@ struct GView {
     if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
       const gptr_u128 v = (gptr_u128)(base + off);
 #pragma unroll
-      for (int j = 0; j < kE / 2; ++j) v[j] = u64x2_t{x[2 * j], x[2 * j + 1]};
+      for (int j = 0; j < kE / 2; ++j) gst<NT>(v + j, u64x2_t{x[2 * j], x[2 * j + 1]});
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) ((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE))[off] = x[j];
+      for (int j = 0; j < kE; ++j) gst<NT>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off, x[j]);
     }
   }
 };
@@ -691,7 +708,7 @@ struct Geo {
 // fwd_range(1, N1, H) q) or kFinalFwd2 (below 2q: HomMult, whose fused row kernel then starts its
 // lazy ranges at 2q and saves two reduction stages -- VALU moved from the VALU-bound fused kernel
 // into the memory-bound column pass).
-template <int LOGN, bool FWD, int H = 8, bool TILED = false, int CFIN = kNotFinal>
+template <int LOGN, bool FWD, int H = 8, bool TILED = false, int CFIN = kNotFinal, bool NTG = false>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_ntt_col(const u64* __restrict__ src,
                                                       const u64* __restrict__ src2,
@@ -722,7 +739,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   if (it >= items) return;
   Item cur = decode(it);
   u64 x[kE], y[kE];
-  pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(cur.s), sub}, t, x);
+  pass_load<G::N1, FWD>(GView<G::R2, NTG>{const_cast<u64*>(cur.s), sub}, t, x);
   while (true) {
     const u32 nx = it + gridDim.x;
     const bool more = kLoopCol && FWD && nx < items;
@@ -735,7 +752,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       nf0 = nfold[4 * cur.limb];
       nf1 = nfold[4 * cur.limb + 1];
     }
-    using GOut = GView<TILED ? G::SUBS_C : G::R2>;
+    using GOut = GView<TILED ? G::SUBS_C : G::R2, NTG>;
     pass_run<G::N1, FWD, FWD ? CFIN : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
         x, GOut{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
         nf0, nf1, prefetch);
@@ -834,6 +851,10 @@ struct HmGeo {
 // range (11q at 16q headroom) carries into the fused kernel.  Measured: column-forward +11 %
 // (114 -> 126 us: it is not VALU-idle enough to absorb 3 subtractions per element), fused kernel
 // unchanged within noise.  Off; kept as an A/B switch.
+#ifndef FHE_HM_NT
+#define FHE_HM_NT 1
+#endif
+constexpr bool kHmNT = FHE_HM_NT != 0;
 #ifndef FHE_HM_COL_REDUCE
 #define FHE_HM_COL_REDUCE 0
 #endif
@@ -896,7 +917,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
                                           (u64)row * G::SUBS_C};
         gin.template load<Lay>(v, tp);
       } else {
-        const GView<1> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
+        const GView<1, kHmNT> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
         gin.template load<Lay>(v, tp);
       }
     } else {
@@ -953,7 +974,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
     }
     if (active) round_compute<G::N2, KB, LO, false, kNotFinal, true>(v, tp, ti, base, q, {0, 0}, {0, 0});
     if constexpr (k == Rd::NR - 1) {
-      const GView<1> gout{d + ((u64)b * 3 + grp) * limbN + loc, 0};
+      const GView<1, kHmNT> gout{d + ((u64)b * 3 + grp) * limbN + loc, 0};
       if (active) gout.template store<Lay>(v, tp);
     } else {
       // the first store into this slot must wait until every group has read it for the tensor
@@ -1322,9 +1343,10 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   prof_mark(s, "hm_row_tensor");
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
-  k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, false>(c, G::THR_C, ii), G::THR_C, 0, s>>>(
-      d, nullptr, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv, c->d_nfold + 2,
-      c->d_mods);
+  k_ntt_col<LOGN, false, 8, false, kNotFinal, kHmNT>
+      <<<item_grid<k_ntt_col<LOGN, false, 8, false, kNotFinal, kHmNT>, false>(c, G::THR_C, ii),
+         G::THR_C, 0, s>>>(d, nullptr, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv,
+                           c->d_nfold + 2, c->d_mods);
   prof_mark(s, "hm_col_inv");
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;
