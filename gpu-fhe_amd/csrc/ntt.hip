@@ -511,7 +511,7 @@ __device__ __forceinline__ void gst(P p, V v) {
   else
     *p = v;
 }
-template <int STRIDE, bool NT = false>
+template <int STRIDE, bool NT = false, bool NTS = NT>
 struct GView {
   u64* base;
   u32 lane;
@@ -537,10 +537,10 @@ struct GView {
     if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
       const gptr_u128 v = (gptr_u128)(base + off);
 #pragma unroll
-      for (int j = 0; j < kE / 2; ++j) gst<NT>(v + j, u64x2_t{x[2 * j], x[2 * j + 1]});
+      for (int j = 0; j < kE / 2; ++j) gst<NTS>(v + j, u64x2_t{x[2 * j], x[2 * j + 1]});
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) gst<NT>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off, x[j]);
+      for (int j = 0; j < kE; ++j) gst<NTS>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off, x[j]);
     }
   }
 };
@@ -708,7 +708,8 @@ struct Geo {
 // fwd_range(1, N1, H) q) or kFinalFwd2 (below 2q: HomMult, whose fused row kernel then starts its
 // lazy ranges at 2q and saves two reduction stages -- VALU moved from the VALU-bound fused kernel
 // into the memory-bound column pass).
-template <int LOGN, bool FWD, int H = 8, bool TILED = false, int CFIN = kNotFinal, bool NTG = false>
+template <int LOGN, bool FWD, int H = 8, bool TILED = false, int CFIN = kNotFinal,
+          bool NTL = false, bool NTS = false>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_ntt_col(const u64* __restrict__ src,
                                                       const u64* __restrict__ src2,
@@ -739,7 +740,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   if (it >= items) return;
   Item cur = decode(it);
   u64 x[kE], y[kE];
-  pass_load<G::N1, FWD>(GView<G::R2, NTG>{const_cast<u64*>(cur.s), sub}, t, x);
+  pass_load<G::N1, FWD>(GView<G::R2, NTL>{const_cast<u64*>(cur.s), sub}, t, x);
   while (true) {
     const u32 nx = it + gridDim.x;
     const bool more = kLoopCol && FWD && nx < items;
@@ -752,7 +753,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       nf0 = nfold[4 * cur.limb];
       nf1 = nfold[4 * cur.limb + 1];
     }
-    using GOut = GView<TILED ? G::SUBS_C : G::R2, NTG>;
+    using GOut = GView<TILED ? G::SUBS_C : G::R2, false, NTS>;
     pass_run<G::N1, FWD, FWD ? CFIN : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
         x, GOut{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
         nf0, nf1, prefetch);
@@ -766,7 +767,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
 
 // Row pass over items (l, p, tile): the limb follows the XCD and the poly varies fastest, so the
 // workgroups of one XCD reuse a row's twiddles while they are hot.
-template <int LOGN, bool FWD, int H = 8>
+template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false>
 __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
                                                       u64* __restrict__ dst, u32 nlimbs,
                                                       u32 limb0, PolyMap pm, u32 items,
@@ -796,7 +797,7 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
   if (it >= items) return;
   Item cur = decode(it);
   u64 x[kE], y[kE];
-  pass_load<G::N2, FWD>(GView<1>{const_cast<u64*>(src) + cur.src, lane}, t, x);
+  pass_load<G::N2, FWD>(GView<1, NTL>{const_cast<u64*>(src) + cur.src, lane}, t, x);
   while (true) {
     const u32 nx = it + gridDim.x;
     const bool more = kLoopRow && nx < items;
@@ -806,7 +807,7 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
     };
     pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, kLoopRow, H,
              fwd_range(1, G::N1, H)>(
-        x, GView<1>{dst + cur.dst, lane}, lv, t, tw_all + (u64)cur.limb * N,
+        x, GView<1, false, NTS>{dst + cur.dst, lane}, lv, t, tw_all + (u64)cur.limb * N,
 #if FHE_NTT_ABLATE == 3  // timing-only build: every row uses row 0's twiddles (cache-resident)
         (u32)G::R1,
 #else
@@ -855,6 +856,19 @@ struct HmGeo {
 #define FHE_HM_NT 1
 #endif
 constexpr bool kHmNT = FHE_HM_NT != 0;
+// FHE_HM_COLF_NTL: the column-forward pass reads a and b non-temporally (read once; +0.7 %).
+#ifndef FHE_HM_COLF_NTL
+#define FHE_HM_COLF_NTL 1
+#endif
+// FHE_NTT_NT_IN / FHE_NTT_NT_OUT: standalone NTT -- first pass's loads / second pass's stores
+// non-temporal.  Measured slower (-8 % / -5 % NTT/s with the bench's back-to-back transforms of
+// one 256 MiB batch, which the Infinity Cache partly holds); off, kept as A/B switches.
+#ifndef FHE_NTT_NT_IN
+#define FHE_NTT_NT_IN 0
+#endif
+#ifndef FHE_NTT_NT_OUT
+#define FHE_NTT_NT_OUT 0
+#endif
 #ifndef FHE_HM_COL_REDUCE
 #define FHE_HM_COL_REDUCE 0
 #endif
@@ -1267,14 +1281,15 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
   using G = Geo<LOGN>;
   const u64 ir = (u64)polys * nlimbs * G::TILES_R;
   const PolyMap pm{1, sp, 0, dp, 0, 0};
-  if (fwd)
-    k_ntt_row<LOGN, true, HD><<<item_grid<k_ntt_row<LOGN, true, HD>, kLoopRow>(c, G::THR_R, ir),
-                                G::THR_R, 0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir,
-                                                  c->d_tw_fwd, c->d_mods);
-  else
-    k_ntt_row<LOGN, false><<<item_grid<k_ntt_row<LOGN, false>, kLoopRow>(c, G::THR_R, ir),
-                             G::THR_R, 0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv,
-                                               c->d_mods);
+  constexpr bool IN = FHE_NTT_NT_IN != 0, OUT = FHE_NTT_NT_OUT != 0;
+  if (fwd)  // the forward's second pass
+    k_ntt_row<LOGN, true, HD, false, OUT>
+        <<<item_grid<k_ntt_row<LOGN, true, HD, false, OUT>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
+           0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_fwd, c->d_mods);
+  else  // the inverse's first pass
+    k_ntt_row<LOGN, false, 8, IN, false>
+        <<<item_grid<k_ntt_row<LOGN, false, 8, IN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
+           0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv, c->d_mods);
 }
 
 #if !FHE_NTT_ROW_ONLY && !FHE_NTT_KS_ONLY
@@ -1303,17 +1318,22 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   // the second pass runs in place on dst
   const PolyMap pd = flat_map(dpstride);
   const u64 ic = pl * G::TILES_C;
+  constexpr bool IN = FHE_NTT_NT_IN != 0, OUT = FHE_NTT_NT_OUT != 0;
   if (fwd) {
-    k_ntt_col<LOGN, true, HD><<<item_grid<k_ntt_col<LOGN, true, HD>, kLoopCol>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
-        src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd, c->d_nfold, c->d_mods);
+    k_ntt_col<LOGN, true, HD, false, kNotFinal, IN, false>
+        <<<item_grid<k_ntt_col<LOGN, true, HD, false, kNotFinal, IN, false>, kLoopCol>(c, G::THR_C, ic),
+           G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd,
+                             c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_fwd");
     row_pass_any<LOGN, HD>(c, true, dst, dpstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_fwd");
   } else {
     row_pass_any<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_inv");
-    k_ntt_col<LOGN, false><<<item_grid<k_ntt_col<LOGN, false>, false>(c, G::THR_C, ic), G::THR_C, 0, s>>>(
-        dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv, c->d_nfold, c->d_mods);
+    k_ntt_col<LOGN, false, 8, false, kNotFinal, false, OUT>
+        <<<item_grid<k_ntt_col<LOGN, false, 8, false, kNotFinal, false, OUT>, false>(c, G::THR_C, ic),
+           G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv,
+                             c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_inv");
   }
   FHE_HIP_CHECK(hipGetLastError());
@@ -1333,7 +1353,8 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   const u64 ic = (u64)batch * 4 * nlimbs * G::TILES_C;
   constexpr bool TL = FHE_HM_TILED != 0;
   constexpr int CF = FHE_HM_COL_REDUCE ? kFinalFwd2 : kNotFinal;
-  k_ntt_col<LOGN, true, HD, TL, CF><<<item_grid<k_ntt_col<LOGN, true, HD, TL, CF>, kLoopCol>(c, G::THR_C, ic),
+  constexpr bool FL = FHE_HM_COLF_NTL != 0;
+  k_ntt_col<LOGN, true, HD, TL, CF, FL><<<item_grid<k_ntt_col<LOGN, true, HD, TL, CF, FL>, kLoopCol>(c, G::THR_C, ic),
                                   G::THR_C, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic,
                                                     c->d_tw_fwd, c->d_nfold, c->d_mods);
   prof_mark(s, "hm_col_fwd");
@@ -1343,8 +1364,8 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   prof_mark(s, "hm_row_tensor");
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
-  k_ntt_col<LOGN, false, 8, false, kNotFinal, kHmNT>
-      <<<item_grid<k_ntt_col<LOGN, false, 8, false, kNotFinal, kHmNT>, false>(c, G::THR_C, ii),
+  k_ntt_col<LOGN, false, 8, false, kNotFinal, kHmNT, kHmNT>
+      <<<item_grid<k_ntt_col<LOGN, false, 8, false, kNotFinal, kHmNT, kHmNT>, false>(c, G::THR_C, ii),
          G::THR_C, 0, s>>>(d, nullptr, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv,
                            c->d_nfold + 2, c->d_mods);
   prof_mark(s, "hm_col_inv");
