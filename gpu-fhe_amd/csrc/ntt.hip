@@ -860,6 +860,12 @@ constexpr bool kHmNT = FHE_HM_NT != 0;
 #ifndef FHE_HM_COLF_NTL
 #define FHE_HM_COLF_NTL 1
 #endif
+// FHE_KS_NT: the key-switch's extended rows (written by k_modup_col, read once by k_ks_row_inner)
+// go through non-temporal stores and loads (fused row kernel 403 -> 379 us per step, +1.5 %).
+#ifndef FHE_KS_NT
+#define FHE_KS_NT 1
+#endif
+constexpr bool kKsNT = FHE_KS_NT != 0;
 // FHE_NTT_NT_IN / FHE_NTT_NT_OUT: standalone NTT -- first pass's loads / second pass's stores
 // non-temporal.  Measured slower (-8 % / -5 % NTT/s with the bench's back-to-back transforms of
 // one 256 MiB batch, which the Infinity Cache partly holds); off, kept as A/B switches.
@@ -1054,7 +1060,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     x[j] = csub(mont_reduce_lazy((u64)acc, (u64)(acc >> 64), m.q, m.qinv), m.q);
   }
   pass_run<G::N1, true, kNotFinal, kBlockSync, false, false, H, 1>(
-      x, GView<G::R2>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
+      x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
       tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
 }
 
@@ -1191,7 +1197,7 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
         using Lay = Layout<G::N2, KB, LO>;
         const u32 tp = Lay::tpos(t);
         if constexpr (k == 0) {
-          const GView<1> gin{const_cast<u64*>(ext) + (u64)grp * ext_ds + (u64)b * rn + (u64)r * N + loc, 0};
+          const GView<1, kKsNT> gin{const_cast<u64*>(ext) + (u64)grp * ext_ds + (u64)b * rn + (u64)r * N + loc, 0};
           gin.template load<Lay>(v, tp);
         } else {
           lds_sync<SY>();
