@@ -61,6 +61,7 @@ def test_errors_are_reported_not_raised():
         _capi.check(rc, "fhe_gen_moduli")
     # null context / bad window on the device entry points: rejected before any HIP call
     assert lib.fhe_ntt_fwd(None, None, 1, 0, 1, None) == -1
+    assert lib.fhe_ntt_inv_to(None, None, None, 1, 0, 1, None) == -1
     assert lib.fhe_vec_add(None, None, None, None, 1, 0, 1, None) == -1
     assert lib.fhe_hommult_workspace(None, 1, 1) == 0
 
