@@ -66,18 +66,6 @@ constexpr int kColThreads = FHE_COL_THREADS;
 #ifndef FHE_FOLD_U
 #define FHE_FOLD_U 1
 #endif
-// FHE_HM_TILED: HomMult's column-forward pass writes its workspace tile-major (one contiguous
-// block per workgroup) and the fused row kernel reads it so (k_ntt_col TILED, TView).  Measured
-// neutral to -2 % (hm_col_fwd 116.5 vs 113.3 us): the 128-byte row segments of the flat layout
-// are not what holds the column pass below the HBM copy rate.  Kept as an A/B switch.
-#ifndef FHE_HM_TILED
-#define FHE_HM_TILED 0
-#endif
-// FHE_SUB_NOT: the butterflies' 64-bit subtractions as a + k + 1 + ~b (two v_not + one
-// v_lshl_add_u64) instead of a v_sub_co/v_subb_co borrow chain through VCC (2 wait states).
-#ifndef FHE_SUB_NOT
-#define FHE_SUB_NOT 0
-#endif
 #ifndef FHE_HM_POLY_MAJOR
 #define FHE_HM_POLY_MAJOR 1
 #endif
@@ -367,13 +355,9 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         u64 s = shoup_q3_add(x[jj], w.x, w.y, nq, u);
         FHE_OPAQUE(s);
         x[j] = s;
-#if FHE_SUB_NOT
-        x[jj] = sub_plus(u << 1, s, q3 + 1);  // 2u + 3q + 1 + ~s: no borrow chain, no VCC hazard
-#else
         u64 t2 = (u << 1) + q3;
         FHE_OPAQUE(t2);
         x[jj] = t2 - s;
-#endif
 #else
         const u64 u = reduce ? csubk(x[j], qh) : x[j];
         const u64 v = shoup_q3(x[jj], w.x, w.y, nq);
@@ -438,11 +422,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         const u64 u = x[j], v = x[jj];
 #if FHE_BFLY == 2
         // GS: inputs in [0, 3q); sum -> [0, 3q); (u - v + 3q) w -> [0, 3q)
-#if FHE_SUB_NOT
-        const u64 sum = u + v, dif = sub_plus(u, v, q3 + 1);
-#else
         const u64 sum = u + v, dif = u - v + q3;
-#endif
 #elif FHE_BFLY == 1
         const u64 sum = u + v, dif = sub_plus(u, v, q2p1);
 #else
@@ -587,21 +567,6 @@ struct LViewC {
   }
 };
 
-// Global view of one row of a tile-major limb (k_ntt_col<..., TILED>): row position c of row
-// `row` lives at base[(c / S) (R1 S) + row S + c % S]; base = the limb's start + row * S.
-template <int S, int R1>
-struct TView {
-  const u64* base;
-  template <class Lay>
-  __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
-#pragma unroll
-    for (int j = 0; j < kE; ++j) {
-      const u32 c = tp | Lay::jpos(j);
-      x[j] = ((gptr_u64)base)[(c / S) * (R1 * S) + c % S];
-    }
-  }
-};
-
 // Round-0 global load of one sub-transform into registers (issued ahead of the work that needs
 // it: the kernels below prefetch their next item while computing the current one).
 template <int LOGR, bool FWD, class GIn>
@@ -701,15 +666,8 @@ struct Geo {
 // multiple of 8, so an item keeps the XCD (blockIdx % 8) its index maps to.
 
 // Column pass over items (p, l, tile) of src/dst [polys][nlimbs][N] via PolyMap.
-// TILED: dst limb rows are written tile-major -- column tile k (SUBS_C columns x R1 rows) as one
-// contiguous block [k][row][SUBS_C] -- so every workgroup's output is one contiguous run of
-// R1 SUBS_C words (the HomMult workspace; the fused row kernel reads it through TView).
-// CFIN (forward only): the column pass's final reduction, kNotFinal (values below
-// fwd_range(1, N1, H) q) or kFinalFwd2 (below 2q: HomMult, whose fused row kernel then starts its
-// lazy ranges at 2q and saves two reduction stages -- VALU moved from the VALU-bound fused kernel
-// into the memory-bound column pass).
-template <int LOGN, bool FWD, int H = 8, bool TILED = false, int CFIN = kNotFinal,
-          bool NTL = false, bool NTS = false>
+// NTL / NTS: non-temporal loads of the source / stores of the destination (see GView).
+template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_ntt_col(const u64* __restrict__ src,
                                                       const u64* __restrict__ src2,
@@ -732,9 +690,8 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     const u32 tile = it % G::TILES_C, pl = it / G::TILES_C;
     const u32 l = pl % nlimbs, p = pl / nlimbs;
     const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
-    const u64 dloc = TILED ? (u64)l * N + (u64)tile * G::SUBS_C * G::R1 : loc;
     const u64* s = pm.second(p) ? src2 + pm.src2(p) : src + pm.src(p);
-    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), s + loc, dst + pm.dst(p) + dloc};
+    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), s + loc, dst + pm.dst(p) + loc};
   };
   u32 it = blockIdx.x;
   if (it >= items) return;
@@ -753,8 +710,8 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       nf0 = nfold[4 * cur.limb];
       nf1 = nfold[4 * cur.limb + 1];
     }
-    using GOut = GView<TILED ? G::SUBS_C : G::R2, false, NTS>;
-    pass_run<G::N1, FWD, FWD ? CFIN : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
+    using GOut = GView<G::R2, false, NTS>;
+    pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
         x, GOut{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
         nf0, nf1, prefetch);
     if (!more) break;
@@ -847,11 +804,7 @@ struct HmGeo {
   static constexpr int SYNC_ROUND = (POLY_MAJOR || LANES_ROW <= 64) ? kWaveSync : kBlockSync;
 };
 
-// FHE_HM_COL_REDUCE: HomMult's column-forward pass leaves its output below 2q (CFIN kFinalFwd2)
-// and the fused kernel's forward ranges start there (kHmColOut); else the column pass's lazy
-// range (11q at 16q headroom) carries into the fused kernel.  Measured: column-forward +11 %
-// (114 -> 126 us: it is not VALU-idle enough to absorb 3 subtractions per element), fused kernel
-// unchanged within noise.  Off; kept as an A/B switch.
+// FHE_HM_NT: non-temporal workspace reads / output writes in the fused kernel and the column inverse.
 #ifndef FHE_HM_NT
 #define FHE_HM_NT 1
 #endif
@@ -875,11 +828,7 @@ constexpr bool kKsNT = FHE_KS_NT != 0;
 #ifndef FHE_NTT_NT_OUT
 #define FHE_NTT_NT_OUT 0
 #endif
-#ifndef FHE_HM_COL_REDUCE
-#define FHE_HM_COL_REDUCE 0
-#endif
-template <int LOGN, int HR = 8, bool TILED = false,
-          int kHmColOut = FHE_HM_COL_REDUCE ? 2 : fwd_range(1, Geo<LOGN>::N1, HR)>
+template <int LOGN, int HR = 8>
 __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
                                                           u64* __restrict__ d, u32 nlimbs,
                                                           u32 limb0,
@@ -928,18 +877,12 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
     constexpr int KB = Rd::kb(k);
     constexpr int LO = Rd::lo_fwd(k);
     constexpr int F = (k == Rd::NR - 1) ? kFinalFwd2 : kNotFinal;
-    constexpr int RIN = fwd_range(kHmColOut, G::N2 - (LO + KB), HR);
+    constexpr int RIN = fwd_range(fwd_range(1, G::N1, HR), G::N2 - (LO + KB), HR);
     using Lay = Layout<G::N2, KB, LO>;
     const u32 tp = Lay::tpos(t);
     if constexpr (k == 0) {
-      if constexpr (TILED) {
-        const TView<G::SUBS_C, G::R1> gin{x + ((u64)b * 4 + grp) * limbN + (u64)l * N +
-                                          (u64)row * G::SUBS_C};
-        gin.template load<Lay>(v, tp);
-      } else {
-        const GView<1, kHmNT> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
-        gin.template load<Lay>(v, tp);
-      }
+      const GView<1, kHmNT> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
+      gin.template load<Lay>(v, tp);
     } else {
       lds_sync<SY>();
       own.template load<Lay>(v, tp);
@@ -1326,8 +1269,8 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   const u64 ic = pl * G::TILES_C;
   constexpr bool IN = FHE_NTT_NT_IN != 0, OUT = FHE_NTT_NT_OUT != 0;
   if (fwd) {
-    k_ntt_col<LOGN, true, HD, false, kNotFinal, IN, false>
-        <<<item_grid<k_ntt_col<LOGN, true, HD, false, kNotFinal, IN, false>, kLoopCol>(c, G::THR_C, ic),
+    k_ntt_col<LOGN, true, HD, IN, false>
+        <<<item_grid<k_ntt_col<LOGN, true, HD, IN, false>, kLoopCol>(c, G::THR_C, ic),
            G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd,
                              c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_fwd");
@@ -1336,8 +1279,8 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   } else {
     row_pass_any<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_inv");
-    k_ntt_col<LOGN, false, 8, false, kNotFinal, false, OUT>
-        <<<item_grid<k_ntt_col<LOGN, false, 8, false, kNotFinal, false, OUT>, false>(c, G::THR_C, ic),
+    k_ntt_col<LOGN, false, 8, false, OUT>
+        <<<item_grid<k_ntt_col<LOGN, false, 8, false, OUT>, false>(c, G::THR_C, ic),
            G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv,
                              c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_inv");
@@ -1357,21 +1300,19 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   // over the 4 polys of every ciphertext pair (group of 4: slots 0, 1 from a, slots 2, 3 from b)
   const PolyMap to_x{4, 2 * limbN, limbN, 4 * limbN, limbN, 2};
   const u64 ic = (u64)batch * 4 * nlimbs * G::TILES_C;
-  constexpr bool TL = FHE_HM_TILED != 0;
-  constexpr int CF = FHE_HM_COL_REDUCE ? kFinalFwd2 : kNotFinal;
   constexpr bool FL = FHE_HM_COLF_NTL != 0;
-  k_ntt_col<LOGN, true, HD, TL, CF, FL><<<item_grid<k_ntt_col<LOGN, true, HD, TL, CF, FL>, kLoopCol>(c, G::THR_C, ic),
+  k_ntt_col<LOGN, true, HD, FL><<<item_grid<k_ntt_col<LOGN, true, HD, FL>, kLoopCol>(c, G::THR_C, ic),
                                   G::THR_C, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic,
                                                     c->d_tw_fwd, c->d_nfold, c->d_mods);
   prof_mark(s, "hm_col_fwd");
   const dim3 gh((u32)((u64)batch * nlimbs * H::TILES));
-  k_hommult_row<LOGN, HD, TL><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd,
+  k_hommult_row<LOGN, HD><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd,
                                                     c->d_tw_inv, c->d_mods);
   prof_mark(s, "hm_row_tensor");
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
-  k_ntt_col<LOGN, false, 8, false, kNotFinal, kHmNT, kHmNT>
-      <<<item_grid<k_ntt_col<LOGN, false, 8, false, kNotFinal, kHmNT, kHmNT>, false>(c, G::THR_C, ii),
+  k_ntt_col<LOGN, false, 8, kHmNT, kHmNT>
+      <<<item_grid<k_ntt_col<LOGN, false, 8, kHmNT, kHmNT>, false>(c, G::THR_C, ii),
          G::THR_C, 0, s>>>(d, nullptr, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv,
                            c->d_nfold + 2, c->d_mods);
   prof_mark(s, "hm_col_inv");
