@@ -86,6 +86,17 @@ constexpr int kColThreads = FHE_COL_THREADS;
 #define FHE_ITEM_LOOP 0
 #endif
 constexpr bool kLoopCol = (FHE_ITEM_LOOP & 1) != 0, kLoopRow = (FHE_ITEM_LOOP & 2) != 0;
+// FHE_ROW_XOUT: forward row passes (k_ntt_row, k_moddown_row) store their last round in linear
+// order through the LDS (pass_run XOUT): ntt-batch row-forward 20.7 -> 19.0 ms, ModDown finish
+// 255 -> 190 us.  FHE_ROW_XIN: the inverse row pass loads its first round the same way -- measured
+// 3.5 % slower (the loads' partial lines are L1 hits), off.
+#ifndef FHE_ROW_XOUT
+#define FHE_ROW_XOUT 1
+#endif
+#ifndef FHE_ROW_XIN
+#define FHE_ROW_XIN 0
+#endif
+constexpr bool kRowXout = FHE_ROW_XOUT != 0, kRowXin = FHE_ROW_XIN != 0;
 #define FHE_KATTR \
   __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES)))
 
@@ -523,6 +534,26 @@ struct GView {
       for (int j = 0; j < kE; ++j) gst<NTS>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off, x[j]);
     }
   }
+  // Linear store of a row: thread t of the row's TPS threads owns positions 2 t + 2 TPS jj
+  // (+ 0, 1), so each 16-byte store instruction covers 16 TPS contiguous bytes of the row.
+  template <u32 TPS>
+  __device__ __forceinline__ void load_lin(u64 (&x)[kE], u32 t) const {
+    static_assert(STRIDE == 1, "rows only");
+    const gptr_u128 v = (gptr_u128)(base + lane) + t;
+#pragma unroll
+    for (int jj = 0; jj < kE / 2; ++jj) {
+      const u64x2_t w = gld<NT>(v + jj * TPS);
+      x[2 * jj] = w.x;
+      x[2 * jj + 1] = w.y;
+    }
+  }
+  template <u32 TPS>
+  __device__ __forceinline__ void store_lin(const u64 (&x)[kE], u32 t) const {
+    static_assert(STRIDE == 1, "rows only");
+    const gptr_u128 v = (gptr_u128)(base + lane) + t;
+#pragma unroll
+    for (int jj = 0; jj < kE / 2; ++jj) gst<NTS>(v + jj * TPS, u64x2_t{x[2 * jj], x[2 * jj + 1]});
+  }
 };
 
 // LDS view of one sub-transform: position p at s[p * PS + (PAD16 ? p >> 4 : 0)].
@@ -587,8 +618,11 @@ __device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
 // after the previous item's LDS reads).
 // `hook` runs once round 0's twiddle loads are in flight (the item loops' prefetch).
 // H / R0: forward headroom and input range of the pass (fwd_range), in units of q.
+// XOUT: the last round goes out through the LDS in linear order (GView::store_lin) instead of
+// straight from registers, whose last-round positions are E consecutive words per thread, so a
+// direct store instruction writes 16 of every 16 E bytes across 16 E * 64 bytes.
 template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, bool LOOPED, int H, int R0,
-          class GOut, class LV, class Hook = NoHook>
+          bool XOUT = false, class GOut, class LV, class Hook = NoHook>
 __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const LV& lv, u32 t,
                                          const ulonglong2* __restrict__ tw, u32 base, u64 q,
                                          ulonglong2 nf0, ulonglong2 nf1,
@@ -626,7 +660,21 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
       for (int j = 0; j < kE; ++j) acc ^= x[j];
       if (acc == 0x5a5a5a5a5a5a5a5aull) gout.template store<Lay>(x, tp);  // practically never
 #else
-      gout.template store<Lay>(x, tp);
+      if constexpr (XOUT) {
+        constexpr u32 TPS = (1u << LOGR) / kE;
+        lds_sync<SYNC>();
+        lv.template store<Lay>(x, tp);
+        lds_sync<SYNC>();
+#pragma unroll
+        for (int jj = 0; jj < kE / 2; ++jj) {
+          const u32 p = 2 * t + 2 * TPS * jj;
+          x[2 * jj] = lv.s[lv.idx(p)];
+          x[2 * jj + 1] = lv.s[lv.idx(p + 1)];
+        }
+        gout.template store_lin<TPS>(x, t);
+      } else {
+        gout.template store<Lay>(x, tp);
+      }
 #endif
     } else {
       // round 0's store needs a fence only when the previous item's last LDS reads precede it;
@@ -754,7 +802,23 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
   if (it >= items) return;
   Item cur = decode(it);
   u64 x[kE], y[kE];
-  pass_load<G::N2, FWD>(GView<1, NTL>{const_cast<u64*>(src) + cur.src, lane}, t, x);
+  if constexpr (!FWD && kRowXin && !kLoopRow) {
+    // the inverse's round 0 owns E consecutive words per thread: load the row linearly and
+    // redistribute through the LDS (the mirror of pass_run's XOUT store)
+    using Rd = Rounds<G::N2>;
+    using Lay0 = Layout<G::N2, Rd::kb_inv(0), Rd::lo_inv(0)>;
+    GView<1, NTL>{const_cast<u64*>(src) + cur.src, lane}.template load_lin<G::TPS_R>(x, t);
+#pragma unroll
+    for (int jj = 0; jj < kE / 2; ++jj) {
+      const u32 p = 2 * t + 2 * G::TPS_R * jj;
+      lv.s[lv.idx(p)] = x[2 * jj];
+      lv.s[lv.idx(p + 1)] = x[2 * jj + 1];
+    }
+    lds_sync<kWaveSync>();
+    lv.template load<Lay0>(x, Lay0::tpos(t));
+  } else {
+    pass_load<G::N2, FWD>(GView<1, NTL>{const_cast<u64*>(src) + cur.src, lane}, t, x);
+  }
   while (true) {
     const u32 nx = it + gridDim.x;
     const bool more = kLoopRow && nx < items;
@@ -763,7 +827,7 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
       if (more) pass_load<G::N2, FWD>(GView<1>{const_cast<u64*>(src) + nxt.src, lane}, t, y);
     };
     pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, kLoopRow, H,
-             fwd_range(1, G::N1, H)>(
+             fwd_range(1, G::N1, H), FWD && kRowXout>(
         x, GView<1, false, NTS>{dst + cur.dst, lane}, lv, t, tw_all + (u64)cur.limb * N,
 #if FHE_NTT_ABLATE == 3  // timing-only build: every row uses row 0's twiddles (cache-resident)
         (u32)G::R1,
@@ -1032,6 +1096,18 @@ struct FinishView {
       o[j] = u64x2_t{r0, r1};
     }
   }
+  template <u32 TPS>
+  __device__ __forceinline__ void store_lin(const u64 (&x)[kE], u32 t) const {
+    const gptr_u128 a = (gptr_u128)(acc + lane) + t;
+    const gptr_u128 o = (gptr_u128)(out + lane) + t;
+#pragma unroll
+    for (int jj = 0; jj < kE / 2; ++jj) {
+      const u64x2_t av = a[jj * TPS];
+      const u64 r0 = csub(shoup_lazy(av.x + q - x[2 * jj], pinv.x, pinv.y, q), q);
+      const u64 r1 = csub(shoup_lazy(av.y + q - x[2 * jj + 1], pinv.x, pinv.y, q), q);
+      o[jj * TPS] = u64x2_t{r0, r1};
+    }
+  }
 };
 
 template <int LOGN, int H>
@@ -1064,7 +1140,7 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   const FinishView fo{(h ? ks1 : ks0) + ((u64)b * nq + l) * N + rloc,
                       acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc, lane, q,
                       pinv[limb]};
-  pass_run<G::N2, true, kFinalFwd, kWaveSync, true, false, H, fwd_range(1, G::N1, H)>(
+  pass_run<G::N2, true, kFinalFwd, kWaveSync, true, false, H, fwd_range(1, G::N1, H), kRowXout>(
       x, fo, lv, t, tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, q, {0, 0}, {0, 0});
 }
 
