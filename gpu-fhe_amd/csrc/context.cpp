@@ -94,6 +94,32 @@ u32 bitrev(u32 x, u32 bits) {
   return r;
 }
 
+// Row-pass twiddle layout (ntt.hip round_compute, ROWTAB).  The standalone and fused row passes
+// split a row of R2 = 2^N2 points into rounds of at most 2^elog-point butterflies; in the round on
+// the lowest position bits (the forward's last, the inverse's first) thread t of the row owns
+// positions t 2^elog + [0, 2^elog), so at row stage st (bit b = N2 - 1 - st) it needs groups
+// g = t W + sj, W = 2^(elog - b - 1), sj < W.  Those stages' segments [(R1 + r) 2^st, +2^st) of
+// every limb's table are stored transposed -- entry g at sj TPS + t, TPS = R2 / 2^elog -- so one
+// twiddle load instruction reads consecutive words across the wavefront's lanes.
+void lane_major_rows(std::vector<ulonglong2>& tw, u32 log_n, int elog) {
+  const u32 n = 1u << log_n;
+  const int n1 = (int)log_n / 2, n2 = (int)log_n - n1;
+  const int nr = (n2 + elog - 1) / elog;
+  const int kb_last = n2 / nr + (nr - 1 < n2 % nr ? 1 : 0);
+  const u32 r1 = 1u << n1, tps = 1u << (n2 - elog);
+  std::vector<ulonglong2> seg;
+  for (size_t base = 0; base < tw.size(); base += n)
+    for (int b = 0; b < kb_last; ++b) {
+      const int st = n2 - 1 - b;
+      const u32 w = 1u << (elog - b - 1), len = 1u << st;
+      for (u32 r = 0; r < r1; ++r) {
+        ulonglong2* p = tw.data() + base + ((size_t)(r1 + r) << st);
+        seg.assign(p, p + len);
+        for (u32 g = 0; g < len; ++g) p[(g % w) * tps + g / w] = seg[g];
+      }
+    }
+}
+
 inline ulonglong2 shoup_pair(u64 w, u64 q) {
   ulonglong2 p;
   p.x = w;
@@ -245,10 +271,17 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
     nfold[4 * i + 2] = shoup_pair(mulmod_u64(n_inv, r_mod, m), m);  // HomMult: undo R^-1
     nfold[4 * i + 3] = shoup_pair(mulmod_u64(nf1, r_mod, m), m);
   }
+  std::vector<ulonglong2> twf8 = twf, twi8 = twi;
+  lane_major_rows(twf, log_n, 4);
+  lane_major_rows(twi, log_n, 4);
+  lane_major_rows(twf8, log_n, 3);
+  lane_major_rows(twi8, log_n, 3);
   int rc = kOk;
   if ((rc = upload(&c->d_mods, c->mods_host.data(), M)) ||
       (rc = upload(&c->d_tw_fwd, twf.data(), M * n)) ||
       (rc = upload(&c->d_tw_inv, twi.data(), M * n)) ||
+      (rc = upload(&c->d_tw_fwd8, twf8.data(), M * n)) ||
+      (rc = upload(&c->d_tw_inv8, twi8.data(), M * n)) ||
       (rc = upload(&c->d_nfold, nfold.data(), 4 * M)) || (rc = build_rns_tables(c)) ||
       (rc = build_galois_tables(c))) {
     ctx_destroy(c);
@@ -264,7 +297,8 @@ int ctx_destroy(fhe_ctx* c) {
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   if (c->aux_fork) (void)hipEventDestroy(c->aux_fork);
   if (c->aux_join) (void)hipEventDestroy(c->aux_join);
-  for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_inv, (void*)c->d_nfold,
+  for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_inv, (void*)c->d_tw_fwd8,
+                    (void*)c->d_tw_inv8, (void*)c->d_nfold,
                     (void*)c->d_modup_inv, (void*)c->d_modup_hat, (void*)c->d_moddown_inv,
                     (void*)c->d_moddown_hat, (void*)c->d_pinv, (void*)c->d_rs_tab,
                     (void*)c->d_rs_half, c->workspace})

@@ -42,6 +42,11 @@ struct fhe_ctx {
   fhe::ModParams* d_mods = nullptr;  // [L + K]
   ulonglong2* d_tw_fwd = nullptr;    // [L + K][N] (psi^brv(k), Shoup)
   ulonglong2* d_tw_inv = nullptr;    // [L + K][N] (psi^-brv(k), Shoup)
+  // The row-pass stages of both tables are stored lane-major for the E = 16 kernels' low-bit round
+  // (context.cpp lane_major_rows); the E = 8 row passes (ntt_row_e8.hip) read these copies, which
+  // are permuted for their own layout.
+  ulonglong2* d_tw_fwd8 = nullptr;
+  ulonglong2* d_tw_inv8 = nullptr;
   // [L + K][4] Shoup pairs: N^-1, psi^-1 N^-1 (last inverse stage), and the same times
   // R = 2^64 (HomMult's inverse, undoing the Montgomery tensor's R^-1)
   ulonglong2* d_nfold = nullptr;

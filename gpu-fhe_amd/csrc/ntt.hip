@@ -307,8 +307,10 @@ constexpr int fwd_range(int r0, int stages, int H) {
 // GATHER = false leaves the twiddle loads to the scheduler, next to their butterflies (better for
 // the column pass, whose twiddles are few and shared); true issues them all first (the row passes:
 // per-lane twiddles from L2, whose latency then overlaps instead of stalling each stage).
+// ROWTAB: the twiddles come from a row table region (base = R1 + row), whose low-bit-round stages
+// are stored lane-major.
 template <int LOGR, int KB, int LO, bool FWD, int FIN, bool GATHER = false, int H = 8,
-          int RIN = 8, class Hook = NoHook>
+          int RIN = 8, bool ROWTAB = GATHER, class Hook = NoHook>
 __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
                                               const ulonglong2* __restrict__ tw, const u32 base,
                                               const u64 q, const ulonglong2 nf0,
@@ -324,13 +326,19 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       constexpr int bitpos = LO + b;
       constexpr int st = LOGR - 1 - bitpos;
       if constexpr (!(FIN == kFinalInv && st == 0)) {  // the last inverse stage folds N^-1 instead
-        const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(TS::T.rep_j[sl]) >> (bitpos + 1));
+        // natural group index: g = t W + sj, W = 2^(kElog - bitpos - 1) (the low-bit round has
+        // tp = t << kElog); the row tables store those stages lane-major (context.cpp
+        // lane_major_rows), so the load index is sj TPS + t and a wavefront reads contiguous words
+        const u32 sj = Lay::jpos(TS::T.rep_j[sl]) >> (bitpos + 1);
+        const u32 g = (ROWTAB && LO == 0) ? sj * ((1u << LOGR) / E) + (tp >> kElog)
+                                          : (tp >> (bitpos + 1)) | sj;
         tws[sl] = ld_tw(tw + (base << st) + g);
       }
     });
     asm volatile("" ::: "memory");
   }
   hook();
+  static_assert(GATHER || !(ROWTAB && LO == 0), "lane-major row twiddles are gathered");
   auto twiddle = [&](int b, int j, int bitpos, int st) {
     if constexpr (GATHER) return tws[TS::T.slot[b][j]];
     const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(j) >> (bitpos + 1));
@@ -649,8 +657,8 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     const ulonglong2* twk = tw;
     if constexpr (LOOPED || GATHER) asm volatile("" : "+s"(twk));
     if constexpr (k == 0)
-      round_compute<LOGR, KB, LO, FWD, F, GATHER || LOOPED, H, RIN>(x, tp, twk, base, q, nf0, nf1,
-                                                                   hook);
+      round_compute<LOGR, KB, LO, FWD, F, GATHER || LOOPED, H, RIN, GATHER>(x, tp, twk, base, q,
+                                                                           nf0, nf1, hook);
     else
       round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN>(x, tp, twk, base, q, nf0, nf1);
 #endif
@@ -1307,14 +1315,17 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
   const u64 ir = (u64)polys * nlimbs * G::TILES_R;
   const PolyMap pm{1, sp, 0, dp, 0, 0};
   constexpr bool IN = FHE_NTT_NT_IN != 0, OUT = FHE_NTT_NT_OUT != 0;
+  static_assert(kElog == 3 || kElog == 4, "row twiddle tables exist for E = 8 and E = 16");
+  const ulonglong2* twf = kElog == 3 ? c->d_tw_fwd8 : c->d_tw_fwd;
+  const ulonglong2* twi = kElog == 3 ? c->d_tw_inv8 : c->d_tw_inv;
   if (fwd)  // the forward's second pass
     k_ntt_row<LOGN, true, HD, false, OUT>
         <<<item_grid<k_ntt_row<LOGN, true, HD, false, OUT>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
-           0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_fwd, c->d_mods);
+           0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, twf, c->d_mods);
   else  // the inverse's first pass
     k_ntt_row<LOGN, false, 8, IN, false>
         <<<item_grid<k_ntt_row<LOGN, false, 8, IN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
-           0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv, c->d_mods);
+           0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, twi, c->d_mods);
 }
 
 #if !FHE_NTT_ROW_ONLY && !FHE_NTT_KS_ONLY
