@@ -271,17 +271,12 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
     nfold[4 * i + 2] = shoup_pair(mulmod_u64(n_inv, r_mod, m), m);  // HomMult: undo R^-1
     nfold[4 * i + 3] = shoup_pair(mulmod_u64(nf1, r_mod, m), m);
   }
-  std::vector<ulonglong2> twf8 = twf, twi8 = twi;
   lane_major_rows(twf, log_n, 4);
   lane_major_rows(twi, log_n, 4);
-  lane_major_rows(twf8, log_n, 3);
-  lane_major_rows(twi8, log_n, 3);
   int rc = kOk;
   if ((rc = upload(&c->d_mods, c->mods_host.data(), M)) ||
       (rc = upload(&c->d_tw_fwd, twf.data(), M * n)) ||
       (rc = upload(&c->d_tw_inv, twi.data(), M * n)) ||
-      (rc = upload(&c->d_tw_fwd8, twf8.data(), M * n)) ||
-      (rc = upload(&c->d_tw_inv8, twi8.data(), M * n)) ||
       (rc = upload(&c->d_nfold, nfold.data(), 4 * M)) || (rc = build_rns_tables(c)) ||
       (rc = build_galois_tables(c))) {
     ctx_destroy(c);
@@ -297,8 +292,7 @@ int ctx_destroy(fhe_ctx* c) {
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   if (c->aux_fork) (void)hipEventDestroy(c->aux_fork);
   if (c->aux_join) (void)hipEventDestroy(c->aux_join);
-  for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_inv, (void*)c->d_tw_fwd8,
-                    (void*)c->d_tw_inv8, (void*)c->d_nfold,
+  for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_inv, (void*)c->d_nfold,
                     (void*)c->d_modup_inv, (void*)c->d_modup_hat, (void*)c->d_moddown_inv,
                     (void*)c->d_moddown_hat, (void*)c->d_pinv, (void*)c->d_rs_tab,
                     (void*)c->d_rs_half, c->workspace})

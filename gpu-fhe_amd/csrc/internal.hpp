@@ -42,11 +42,8 @@ struct fhe_ctx {
   fhe::ModParams* d_mods = nullptr;  // [L + K]
   ulonglong2* d_tw_fwd = nullptr;    // [L + K][N] (psi^brv(k), Shoup)
   ulonglong2* d_tw_inv = nullptr;    // [L + K][N] (psi^-brv(k), Shoup)
-  // The row-pass stages of both tables are stored lane-major for the E = 16 kernels' low-bit round
-  // (context.cpp lane_major_rows); the E = 8 row passes (ntt_row_e8.hip) read these copies, which
-  // are permuted for their own layout.
-  ulonglong2* d_tw_fwd8 = nullptr;
-  ulonglong2* d_tw_inv8 = nullptr;
+  // (both tables: the row-pass stages of the low-bit round are stored lane-major, context.cpp
+  // lane_major_rows)
   // [L + K][4] Shoup pairs: N^-1, psi^-1 N^-1 (last inverse stage), and the same times
   // R = 2^64 (HomMult's inverse, undoing the Montgomery tensor's R^-1)
   ulonglong2* d_nfold = nullptr;
@@ -79,10 +76,6 @@ int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 pol
 // the same with separate source / destination poly strides
 int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
                        u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
-// Row pass only, from ntt_row_e8.hip (ntt.hip rebuilt with 8 elements per thread): the second
-// pass of a forward / first pass of an inverse standalone NTT.
-int launch_ntt_row_e8(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
-                      u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
 // Column-forward pass only (first half of a forward NTT; the key-switch's fused row kernel
 // finishes it).
 int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,

@@ -31,12 +31,10 @@
 namespace fhe {
 namespace {
 
-// FHE_ELOG: log2 of the elements a thread holds per round (16 -> rounds of up to 4 stages;
-// 8 -> rounds of up to 3 stages, half the LDS and VGPRs per wave, twice the waves per CU).
-#ifndef FHE_ELOG
-#define FHE_ELOG 4
-#endif
-constexpr int kElog = FHE_ELOG;
+// log2 of the elements a thread holds per round: 16, rounds of up to 4 stages.  (E = 8 standalone
+// row passes measured faster until their stores and twiddle loads were made contiguous, then 10 %
+// slower; context.cpp lane_major_rows lays the row twiddles out for this E.)
+constexpr int kElog = 4;
 constexpr int kE = 1 << kElog;
 constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per workgroup
 // FHE_COL_THREADS: column-pass workgroup size; more threads = wider tiles (16 columns per 256
@@ -1315,9 +1313,8 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
   const u64 ir = (u64)polys * nlimbs * G::TILES_R;
   const PolyMap pm{1, sp, 0, dp, 0, 0};
   constexpr bool IN = FHE_NTT_NT_IN != 0, OUT = FHE_NTT_NT_OUT != 0;
-  static_assert(kElog == 3 || kElog == 4, "row twiddle tables exist for E = 8 and E = 16");
-  const ulonglong2* twf = kElog == 3 ? c->d_tw_fwd8 : c->d_tw_fwd;
-  const ulonglong2* twi = kElog == 3 ? c->d_tw_inv8 : c->d_tw_inv;
+  const ulonglong2* twf = c->d_tw_fwd;
+  const ulonglong2* twi = c->d_tw_inv;
   if (fwd)  // the forward's second pass
     k_ntt_row<LOGN, true, HD, false, OUT>
         <<<item_grid<k_ntt_row<LOGN, true, HD, false, OUT>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
@@ -1328,23 +1325,7 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
            0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, twi, c->d_mods);
 }
 
-#if !FHE_NTT_ROW_ONLY && !FHE_NTT_KS_ONLY
-// FHE_ROW_E8: the standalone row passes come from ntt_row_e8.hip, this file rebuilt with E = 8
-// elements per thread (half the VGPRs and LDS per wave: twice the resident waves to hide the row
-// twiddles' L2 latency; measured row-forward -9 %, row-inverse -2 %).  The fused HomMult kernel
-// and the column passes keep E = 16 (the fused kernel is 21 % slower at E = 8).
-#ifndef FHE_ROW_E8
-#define FHE_ROW_E8 1
-#endif
-template <int LOGN, int HD>
-void row_pass_any(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 dp,
-                  u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
-  if (FHE_ROW_E8)
-    launch_ntt_row_e8(c, fwd, src, sp, dst, dp, polys, limb0, nlimbs, s);
-  else
-    row_pass<LOGN, HD>(c, fwd, src, sp, dst, dp, polys, limb0, nlimbs, s);
-}
-
+#if !FHE_NTT_KS_ONLY
 template <int LOGN, int HD>
 int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* dst,
                  u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
@@ -1361,10 +1342,10 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
            G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd,
                              c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_fwd");
-    row_pass_any<LOGN, HD>(c, true, dst, dpstride, dst, dpstride, polys, limb0, nlimbs, s);
+    row_pass<LOGN, HD>(c, true, dst, dpstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_fwd");
   } else {
-    row_pass_any<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
+    row_pass<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_inv");
     k_ntt_col<LOGN, false, 8, false, OUT>
         <<<item_grid<k_ntt_col<LOGN, false, 8, false, OUT>, false>(c, G::THR_C, ic),
@@ -1406,30 +1387,13 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;
 }
-#endif  // !FHE_NTT_ROW_ONLY
+#endif  // !FHE_NTT_KS_ONLY
 
 }  // namespace
 
 #define FHE_LOGN_CASES(X) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17)
 
-#if FHE_NTT_ROW_ONLY
-int launch_ntt_row_e8(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
-                      u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
-  switch (c->log_n) {
-#define X(n)                                                                                  \
-  case n:                                                                                     \
-    if (c->lz16)                                                                              \
-      row_pass<n, 16>(c, forward, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);    \
-    else                                                                                      \
-      row_pass<n, 8>(c, forward, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);     \
-    return kOk;
-    FHE_LOGN_CASES(X)
-#undef X
-  }
-  set_error("unsupported log_n");
-  return kUnsupported;
-}
-#elif FHE_NTT_KS_ONLY
+#if FHE_NTT_KS_ONLY
 
 namespace {
 template <int LOGN, int HD>
@@ -1637,6 +1601,6 @@ int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 bat
   return kOk;
 }
 
-#endif  // FHE_NTT_ROW_ONLY / FHE_NTT_KS_ONLY
+#endif  // FHE_NTT_KS_ONLY
 
 }  // namespace fhe
