@@ -168,6 +168,34 @@ __device__ __forceinline__ u64 mont_reduce_lazy(u64 tlo, u64 thi, u64 q, u64 qin
   return thi + mulhi64(m, q) + (tlo != 0 ? 1 : 0);
 }
 
+// Sum of up to four products y_k h_k with y_k, h_k < 2^61, from 30-bit pieces (lo = v & (2^30 - 1),
+// hi = v >> 30 < 2^31): the partial products of each weight 1, 2^30, 2^60 sum in one 64-bit word
+// (4 < 2^62, 8 < 2^64, 4 < 2^64) with no carries, so a term costs four v_mad_u64_u32 instead of a
+// 128-bit product and add (the base conversions' inner loop).  mont() recombines the 128-bit sum
+// once and Montgomery-reduces it: sum R^-1 mod q in [0, q), valid while sum < q 2^64.
+constexpr u32 kLo30 = (1u << 30) - 1;
+__device__ __forceinline__ u64 split30(u64 v) { return ((v >> 30) << 32) | (v & kLo30); }
+struct Sum30 {
+  u64 lo = 0, mid = 0, hi = 0;
+  __device__ __forceinline__ void add(u32 yl, u32 yh, u32 hl, u32 hh) {
+    lo = mad_u64_u32(yl, hl, lo);
+    mid = mad_u64_u32(yl, hh, mid);
+    mid = mad_u64_u32(yh, hl, mid);
+    hi = mad_u64_u32(yh, hh, hi);
+  }
+  // h2 = split30(h): hl in the low word, hh in the high word
+  __device__ __forceinline__ void add(u64 y2, u64 h2) {
+    add((u32)y2, (u32)(y2 >> 32), (u32)h2, (u32)(h2 >> 32));
+  }
+  __device__ __forceinline__ u64 mont(u64 q, u64 qinv) const {
+    const u64 a = lo + (mid << 30);
+    u64 h = (mid >> 34) + (a < lo ? 1 : 0);
+    const u64 l = a + (hi << 60);
+    h += (hi >> 4) + (l < a ? 1 : 0);
+    return csub(mont_reduce_lazy(l, h, q, qinv), q);
+  }
+};
+
 // Full reduction of a 128-bit z = (zhi, zlo) with zhi < 2^64 (any value) into [0, q), q < 2^61:
 // zhi 2^64 + zlo = zhi (2^64 mod q) + zlo, both terms by the 3-product Shoup (into [0, 3q) each),
 // then three conditional subtractions.  The key-switch inner product accumulates up to 16

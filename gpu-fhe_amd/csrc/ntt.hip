@@ -1020,7 +1020,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
 // ModUp column pass (key-switch): the column-forward pass of every extended row of one digit,
 // reading its input straight from the digit's S pre-scaled source rows y_k = [x_k (D^_k)^-1]_{d_k}
 // (coefficient form, rns.hip k_modup_scale) and converting on the fly:
-//   x = sum_k y_k (D^_k mod t) mod t   (128-bit sum < S 2^61 t < t 2^64, one Montgomery reduction;
+//   x = sum_k y_k (D^_k mod t) mod t   (sum < S 2^61 t < t 2^64: Sum30, one Montgomery reduction;
 //                                       hat[k hs + t].y = D^_k 2^64 mod t)
 // so the extended rows are never written in coefficient form (SURVEY §8a' ModUp; the unfused path
 // is k_baseconv + k_ntt_col).  Items (target row, ciphertext, column tile) are dealt XCD-major,
@@ -1058,19 +1058,20 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   const u32 r = tr < skip_at ? tr : tr + skip_len;
   const u32 limb = __builtin_amdgcn_readfirstlane(r < n0 ? base0 + r : base1 + (r - n0));
   const ModParams m = mods[limb];
-  u64 hm[S];
+  // the constants' 30-bit pieces (Sum30: four v_mad_u64_u32 per term, 2590 -> 2322 VALU per wave)
+  u64 h2[S];
 #pragma unroll
-  for (int k = 0; k < S; ++k) hm[k] = hat[(u64)k * hs + limb].y;
+  for (int k = 0; k < S; ++k) h2[k] = split30(hat[(u64)k * hs + limb].y);
   const u32 tp = Lay0::tpos(t);
   const gptr_u64 yb = (gptr_u64)(y + (u64)b * S * N + (u64)tile * G::SUBS_C + sub);
   u64 x[kE];
 #pragma unroll
   for (int j = 0; j < kE; ++j) {
     const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
-    u128 acc = 0;
+    Sum30 acc;
 #pragma unroll
-    for (int k = 0; k < S; ++k) acc += (u128)yb[(u64)k * N + i] * hm[k];
-    x[j] = csub(mont_reduce_lazy((u64)acc, (u64)(acc >> 64), m.q, m.qinv), m.q);
+    for (int k = 0; k < S; ++k) acc.add(split30(yb[(u64)k * N + i]), h2[k]);
+    x[j] = acc.mont(m.q, m.qinv);
   }
   pass_run<G::N1, true, kNotFinal, kBlockSync, false, false, H, 1>(
       x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,

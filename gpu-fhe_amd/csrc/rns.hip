@@ -59,12 +59,14 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
   // S < 8: y_k < 2^61 and S 2^61 < 2^64, so the sum stays below t 2^64 and one Montgomery
   // reduction (R = 2^64, folded into the table's second word) replaces reduce128
   constexpr bool kMont = S < 8;
+  // S <= 4: the sums run on 30-bit pieces (Sum30), the LDS holding split30(hat)
+  constexpr bool kSplit = S <= 4;
   __shared__ u64 s_hat[kMaxRows * S];
   __shared__ u32 s_limb[kMaxRows];
   for (u32 e = threadIdx.x; e < T * S; e += blockDim.x) {
     const u32 r = e / S, k = e % S;
     const ulonglong2 h = hat[(u64)k * hs + map.limb(r)];
-    s_hat[e] = kMont ? h.y : h.x;
+    s_hat[e] = kSplit ? split30(h.y) : kMont ? h.y : h.x;
   }
   for (u32 r = threadIdx.x; r < T; r += blockDim.x) s_limb[r] = map.limb(r);
   __syncthreads();
@@ -78,10 +80,19 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
     const u64 qk = mods[src0 + k].q;
     const ulonglong2 w = inv[k];
     y[k] = csub(shoup_lazy(in[(u64)k * n + i], w.x, w.y, qk), qk);
+    if constexpr (kSplit) y[k] = split30(y[k]);
   }
   for (u32 r = 0; r < T; ++r) {
     const u32 limb = s_limb[r];
     if (limb >= skip_lo && limb < skip_hi) continue;
+    if constexpr (kSplit) {
+      Sum30 acc;
+#pragma unroll
+      for (int k = 0; k < S; ++k) acc.add(y[k], s_hat[r * S + k]);
+      const ModParams& m = mods[limb];
+      out[(u64)r * n + i] = acc.mont(m.q, m.qinv);
+      continue;
+    }
     u128 acc = 0;
 #pragma unroll
     for (int k = 0; k < S; ++k) acc += (u128)y[k] * s_hat[r * S + k];
