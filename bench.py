@@ -240,7 +240,10 @@ def run_ntt(args, world, rank):
            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
            # every NTT pass reads and writes each coefficient once
            "roofline": roofline(dom, polys * shard.nlimbs * n * 16, kavg[dom], shape)}
-    return out, None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_ntt(ctx.moduli, args.log_n, args.cpu_seconds)
+    return out, cpu
 
 
 def cpu_baseline_ntt(moduli, log_n, budget_s):
@@ -264,6 +267,31 @@ def cpu_baseline_ntt(moduli, log_n, budget_s):
     return {"value": round(done / dt, 1), "unit": "NTT/s", "cores": threads, "kind": "port",
             "sample": f"{done} forward NTTs (N=2^{log_n}, {len(mods)} limbs x {P} polys per call; "
                       f"exact C restatement oracle/fhe_oracle.c, OpenMP {threads} threads) in {dt:.1f} s"}
+
+
+def cpu_baseline_keyswitch(moduli, special, log_n, dnum, budget_s):
+    """Exact C restatement (oracle/, test infrastructure) timed on this host: key-switches/s, one
+    ciphertext per call (its NTTs and products OpenMP-parallel across limbs)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle  # noqa: E402
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    rng = np.random.default_rng(2)
+    n = 1 << log_n
+    allm = list(moduli) + list(special)
+    d2 = np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in moduli])
+    evk = [np.stack([np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in allm])
+                     for _ in range(dnum)]) for _ in range(2)]
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < budget_s:
+        coracle.keyswitch(d2, evk[0], evk[1], moduli, special, dnum)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 2), "unit": "keyswitch/s", "cores": threads, "kind": "port",
+            "sample": f"{done} key-switches (N=2^{log_n}, L={len(moduli)}, K={len(special)}, "
+                      f"dnum={dnum}; exact C restatement oracle/fhe_oracle.c, OpenMP {threads} "
+                      f"threads) in {dt:.1f} s"}
 
 
 def run_ntt_batch(args, world, rank):
@@ -348,7 +376,10 @@ def run_keyswitch(args, world, rank):
            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
            "roofline": roofline("keyswitch (whole, per GPU)", alg // world, dt / (B * args.steps) * 1e3,
                                 {"log_n": args.log_n, "L": L, "world": world})}
-    return out, None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_keyswitch(ctx.moduli, ctx.special, args.log_n, dnum, args.cpu_seconds)
+    return out, cpu
 
 
 def run_mulrelin(args, world, rank):

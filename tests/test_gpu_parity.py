@@ -191,6 +191,25 @@ def test_hommult_many_limbs_matches_oracle(fc, log_n, L, B):
     assert (d == coracle.hommult(a, b, ctx.moduli)).all()
 
 
+@pytest.mark.parametrize("log_n", [10, 11, 12, 13, 14, 15, 16, 17])
+def test_row_layouts_every_log_n(fc, log_n):
+    """Every transform size's row geometry (rows of 2^5 .. 2^9 points, the lane-major twiddle
+    segments of context.cpp lane_major_rows, the linear row stores): HomMult and the fused
+    key-switch (k_ks_row_inner, k_moddown_row) against the C oracle."""
+    ctx = ctx_for(fc, log_n, 4, K=2, dnum=2)
+    a = rand(ctx.moduli, log_n, (2, 2), seed=80 + log_n)
+    b = rand(ctx.moduli, log_n, (2, 2), seed=90 + log_n)
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    assert (d == coracle.hommult(a, b, ctx.moduli)).all()
+    allm = ctx.all_moduli
+    d2 = rand(ctx.moduli, log_n, seed=100 + log_n)
+    eb = rand(allm, log_n, (2,), seed=101)
+    ea = rand(allm, log_n, (2,), seed=102)
+    ks0, ks1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(eb), fc.to_device(ea))
+    r0, r1 = coracle.keyswitch(d2, eb, ea, ctx.moduli, ctx.special, 2)
+    assert (fc.to_host(ks0) == r0).all() and (fc.to_host(ks1) == r1).all()
+
+
 def test_hommult_small_schoolbook(fc):
     ctx = ctx_for(fc, 10, 2)
     a = rand(ctx.moduli, 10, (2,), seed=4)
