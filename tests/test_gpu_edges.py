@@ -104,3 +104,27 @@ def test_out_of_place_ntt_leaves_source(fc, log_n, L):
     assert (fc.to_host(y) == coracle.ntt_fwd(x, ctx.moduli)).all()
     z = ctx.intt(y)
     assert (fc.to_host(z) == x).all() and (fc.to_host(y) == coracle.ntt_fwd(x, ctx.moduli)).all()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_hommult_rank_shapes_of_the_scaling_bench(fc, world):
+    """The per-rank shape bench.py runs at N = 2 / 8 GPUs (L = 8 limbs sharded, 64 N ciphertext
+    pairs, the last rank's limb window): the whole batch on the GPU, the first and last pairs
+    checked bit-exact against the C oracle."""
+    import torch
+    from fhecore import dist as fdist
+
+    ctx = fc.Context(16, L=8)
+    shard = fdist.LimbShard(8, world, world - 1)
+    mods = ctx.moduli[shard.lo:shard.hi]
+    B = 64 * world
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(world)
+    a = torch.stack([torch.randint(0, q, (B, 2, 1 << 16), generator=gen, dtype=torch.int64,
+                                   device="cuda") for q in mods], 2)
+    b = torch.stack([torch.randint(0, q, (B, 2, 1 << 16), generator=gen, dtype=torch.int64,
+                                   device="cuda") for q in mods], 2)
+    d = fdist.sharded_hommult(ctx, a, b, shard)
+    for sl in (slice(0, 2), slice(B - 2, B)):
+        want = coracle.hommult(fc.to_host(a[sl]), fc.to_host(b[sl]), mods)
+        assert (fc.to_host(d[sl]) == want).all()
