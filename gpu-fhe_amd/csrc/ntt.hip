@@ -39,6 +39,7 @@ constexpr int kE = 1 << kElog;
 constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per workgroup
 // FHE_COL_THREADS: column-pass workgroup size; more threads = wider tiles (16 columns per 256
 // threads at N = 2^16), i.e. longer contiguous runs per row in HBM, at the same LDS per wave.
+// 512 measured: ntt-batch (N = 2^17) column pass -4 %, HomMult column inverse +9 %; 256 kept.
 #ifndef FHE_COL_THREADS
 #define FHE_COL_THREADS kThreads
 #endif
@@ -86,13 +87,14 @@ constexpr int kColThreads = FHE_COL_THREADS;
 constexpr bool kLoopCol = (FHE_ITEM_LOOP & 1) != 0, kLoopRow = (FHE_ITEM_LOOP & 2) != 0;
 // FHE_ROW_XOUT: forward row passes (k_ntt_row, k_moddown_row) store their last round in linear
 // order through the LDS (pass_run XOUT): ntt-batch row-forward 20.7 -> 19.0 ms, ModDown finish
-// 255 -> 190 us.  FHE_ROW_XIN: the inverse row pass loads its first round the same way -- measured
-// 3.5 % slower (the loads' partial lines are L1 hits), off.
+// 255 -> 190 us.  FHE_ROW_XIN: the inverse row pass loads its first round the same way: row
+// inverse 121.5 -> 118.3 us at E = 16 (it was 3.5 % slower at E = 8, where the partial-line loads
+// were L1 hits).
 #ifndef FHE_ROW_XOUT
 #define FHE_ROW_XOUT 1
 #endif
 #ifndef FHE_ROW_XIN
-#define FHE_ROW_XIN 0
+#define FHE_ROW_XIN 1
 #endif
 constexpr bool kRowXout = FHE_ROW_XOUT != 0, kRowXin = FHE_ROW_XIN != 0;
 #define FHE_KATTR \
