@@ -1213,8 +1213,15 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
   u64 v[kE];
   if (grp < (u32)DNUM) {
     if (is_own) {
+      // d2 is already in NTT form: straight into the LDS slot, read in linear order
       const GView<1> gin{const_cast<u64*>(d2_own) + ((u64)b * nq + r) * N + loc, 0};
-      gin.template load<LayT>(v, tpT);
+      gin.template load_lin<H::TPS>(v, t);
+#pragma unroll
+      for (int jj = 0; jj < kE / 2; ++jj) {
+        const u32 p = 2 * t + 2 * H::TPS * jj;
+        own_slot.s[own_slot.idx(p)] = v[2 * jj];
+        own_slot.s[own_slot.idx(p + 1)] = v[2 * jj + 1];
+      }
     } else {
       const ulonglong2* tf = twf + (u64)limb * N;
       static_for<0, Rd::NR>([&](auto kc) {
@@ -1238,9 +1245,9 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
           own_slot.template store<Lay>(v, tp);
         }
       });
+      lds_sync<SY>();
+      own_slot.template store<LayT>(v, tpT);
     }
-    lds_sync<SY>();
-    own_slot.template store<LayT>(v, tpT);
   }
   __syncthreads();
   // combine: the workgroup's ROWS x R2 positions are re-dealt so that each thread takes CW
