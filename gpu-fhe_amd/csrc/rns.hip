@@ -25,6 +25,9 @@ constexpr int kMaxSrc = 16;
 #ifndef FHE_MODUP_FUSED
 #define FHE_MODUP_FUSED 1
 #endif
+#ifndef FHE_MODDOWN_FUSED
+#define FHE_MODDOWN_FUSED 1
+#endif
 
 // out row r -> ctx limb: r < n0 ? base0 + r : base1 + (r - n0)
 struct RowMap {
@@ -172,20 +175,21 @@ __global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ o
   out1[e] = csub(shoup_lazy(acc[acc_ws + ai] + q - c1, w.x, w.y, q), q);
 }
 
-// ModUp prologue for the fused column pass (ntt.hip k_modup_col): y[b][k][i] = [x_k (D^_k)^-1]_{d_k}
-// over the digit's S source rows of c_all [batch][L][N].  Grid: x over coefficients, y = k, z = b.
-__global__ __launch_bounds__(kThreads) void k_modup_scale(const u64* __restrict__ c_all, u64 in_bs,
-                                                          u32 src0, u64* __restrict__ y, u32 S,
+// Prologue of the fused conversion column pass (ntt.hip k_modup_col), ModUp and ModDown:
+// y[b][k][i] = [x_k (D^_k)^-1]_{d_k} over S consecutive source rows in[b][k] (batch stride in_bs)
+// whose moduli are mods[mod0 + k].  Grid: x over coefficients, y = k, z = b.
+__global__ __launch_bounds__(kThreads) void k_modup_scale(const u64* __restrict__ in, u64 in_bs,
+                                                          u32 mod0, u64* __restrict__ y, u32 S,
                                                           u32 log_n,
                                                           const ulonglong2* __restrict__ inv,
                                                           const ModParams* __restrict__ mods) {
   const u64 n = 1ull << log_n;
   const u32 k = blockIdx.y, b = blockIdx.z;
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  const u64 q = mods[src0 + k].q;
+  const u64 q = mods[mod0 + k].q;
   const ulonglong2 w = inv[k];
   y[((u64)b * S + k) * n + i] =
-      csub(shoup_lazy(c_all[(u64)b * in_bs + (u64)(src0 + k) * n + i], w.x, w.y, q), q);
+      csub(shoup_lazy(in[(u64)b * in_bs + (u64)k * n + i], w.x, w.y, q), q);
 }
 
 template <class T>
@@ -356,7 +360,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
     if (fused_up) {
       const u32 S = hi - lo;
       k_modup_scale<<<dim3((u32)(n / kThreads), S, batch), kThreads, 0, s>>>(
-          c_all, (u64)L * n, lo, yws, S, c->log_n, c->d_modup_inv + (size_t)j * alpha, c->d_mods);
+          c_all + (u64)lo * n, (u64)L * n, lo, yws, S, c->log_n, c->d_modup_inv + (size_t)j * alpha,
+          c->d_mods);
       FHE_HIP_CHECK(hipGetLastError());
       // this rank's own rows of digit j are skipped: ks_row_inner takes them from d2_own
       const u32 own_lo = std::max(lo, limb0), own_hi = std::min(hi, limb0 + nlimbs);
@@ -399,6 +404,24 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   // ModDown: INTT the P rows of both accumulators, convert P -> own Q-limbs, NTT, finish
   u64* accp = acc + (u64)nlimbs * n;
   if ((rc = launch_ntt(c, false, accp, accp, 2 * batch, rn, L, K, s))) return rc;
+  // FHE_MODDOWN_FUSED (fused path, K <= 4): the P -> Q conversion runs inside the column-forward
+  // pass of the conversion NTT (k_modup_col, as ModUp), after scaling the P rows into the ext
+  // region (free once the inner product has run): conv is never written in coefficient form.
+  if (fused && FHE_MODDOWN_FUSED && K <= 4 && (u64)c->dnum * rows >= 2 * (u64)K) {
+    u64* ydn = ext;  // [2 batch][K][N]
+    k_modup_scale<<<dim3((u32)(n / kThreads), K, 2 * batch), kThreads, 0, s>>>(
+        accp, rn, L, ydn, K, c->log_n, c->d_moddown_inv, c->d_mods);
+    FHE_HIP_CHECK(hipGetLastError());
+    prof_mark(s, "ks_moddown_conv");
+    const ModUpColArgs md{ydn, conv, (u64)nlimbs * n, K, nlimbs, nlimbs, 0, nlimbs, limb0, 0,
+                          2 * batch, c->d_moddown_hat, M};
+    if ((rc = launch_modup_col(c, md, s))) return rc;
+    prof_mark(s, "ks_moddown_col");
+    const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch};
+    if ((rc = launch_moddown_row(c, da, s))) return rc;
+    prof_mark(s, "moddown_row_finish");
+    return kOk;
+  }
   const BcArgs down{accp, rn, L, conv, (u64)nlimbs * n, nlimbs, RowMap{nlimbs, limb0, 0}, 0, 0,
                     2 * batch};
   if ((rc = baseconv_any(K, down, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, s)))
