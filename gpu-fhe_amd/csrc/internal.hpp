@@ -58,6 +58,9 @@ struct fhe_ctx {
   ulonglong2* d_moddown_inv = nullptr;  // [K]                  (P^_k)^-1 mod p_k
   ulonglong2* d_moddown_hat = nullptr;  // [K][L + K]           P^_k mod q_i
   ulonglong2* d_pinv = nullptr;         // [L]                  P^-1 mod q_i
+  // fold table for ModDown's INTT of the P rows (entries of limbs L..L+K-1): N^-1 (P^_k)^-1 and
+  // psi^-N/2 N^-1 (P^_k)^-1, so the INTT emits the scaled conversion inputs directly
+  ulonglong2* d_nfold_down = nullptr;   // [L + K][4]
 
   void* workspace = nullptr;
   size_t workspace_bytes = 0;
@@ -74,8 +77,10 @@ namespace fhe {
 int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 polys, u64 pstride,
                u32 limb0, u32 nlimbs, hipStream_t s);
 // the same with separate source / destination poly strides
+// (nfold: the inverse's last-stage fold table [limb][4], default c->d_nfold)
 int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
-                       u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
+                       u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s,
+                       const ulonglong2* nfold = nullptr);
 // Column-forward pass only (first half of a forward NTT; the key-switch's fused row kernel
 // finishes it).
 int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,

@@ -1338,7 +1338,8 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
 #if !FHE_NTT_KS_ONLY
 template <int LOGN, int HD>
 int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* dst,
-                 u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
+                 u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s,
+                 const ulonglong2* nfold) {
   using G = Geo<LOGN>;
   const u64 pl = (u64)polys * nlimbs;
   const PolyMap pm{1, spstride, 0, dpstride, 0, 0};
@@ -1360,7 +1361,7 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
     k_ntt_col<LOGN, false, 8, false, OUT>
         <<<item_grid<k_ntt_col<LOGN, false, 8, false, OUT>, false>(c, G::THR_C, ic),
            G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv,
-                             c->d_nfold, c->d_mods);
+                             nfold ? nfold : c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_inv");
   }
   FHE_HIP_CHECK(hipGetLastError());
@@ -1544,15 +1545,16 @@ int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 pol
 }
 
 int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
-                       u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
+                       u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s,
+                       const ulonglong2* nfold) {
   if ((u64)polys * nlimbs == 0) return kOk;
   switch (c->log_n) {
 #define X(n) \
   case n:    \
     return c->lz16 ? ntt_dispatch<n, 16>(c, forward, src, spstride, dst, dpstride, polys, limb0, \
-                                         nlimbs, s)                                            \
+                                         nlimbs, s, nfold)                                     \
                    : ntt_dispatch<n, 8>(c, forward, src, spstride, dst, dpstride, polys, limb0,  \
-                                        nlimbs, s);
+                                        nlimbs, s, nfold);
     FHE_LOGN_CASES(X)
 #undef X
   }

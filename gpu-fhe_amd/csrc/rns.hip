@@ -304,10 +304,19 @@ int build_rns_tables(fhe_ctx* c) {
     for (u32 k = 0; k < K; ++k) pm = mulmod_u64(pm, c->moduli[L + k] % q, q);
     pinv[i] = shoup_pair(powmod_u64(pm, q - 2, q), q);
   }
+  // ModDown's P-row INTT folds the conversion's (P^_k)^-1 into its last stage (N^-1 fold)
+  std::vector<ulonglong2> nf_down((size_t)4 * M, ulonglong2{0, 0});
+  for (u32 k = 0; k < K; ++k) {
+    const u64 p = c->moduli[L + k];
+    const u64 s = mulmod_u64(powmod_u64(c->n % p, p - 2, p), dn_inv[k].x, p);  // N^-1 (P^_k)^-1
+    const u64 w = powmod_u64(powmod_u64(c->psi[L + k], p - 2, p), c->n / 2, p);  // psi^-N/2
+    nf_down[4 * (L + k)] = shoup_pair(s, p);
+    nf_down[4 * (L + k) + 1] = shoup_pair(mulmod_u64(w, s, p), p);
+  }
   int rc;
   if ((rc = upload(&c->d_modup_inv, up_inv)) || (rc = upload(&c->d_modup_hat, up_hat)) ||
       (rc = upload(&c->d_moddown_inv, dn_inv)) || (rc = upload(&c->d_moddown_hat, dn_hat)) ||
-      (rc = upload(&c->d_pinv, pinv)))
+      (rc = upload(&c->d_pinv, pinv)) || (rc = upload(&c->d_nfold_down, nf_down)))
     return rc;
   return kOk;
 }
@@ -403,15 +412,18 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   prof_mark(s, "ks_inner");
   // ModDown: INTT the P rows of both accumulators, convert P -> own Q-limbs, NTT, finish
   u64* accp = acc + (u64)nlimbs * n;
-  if ((rc = launch_ntt(c, false, accp, accp, 2 * batch, rn, L, K, s))) return rc;
+  const bool fused_down = fused && FHE_MODDOWN_FUSED && K <= 4 && (u64)c->dnum * rows >= 2 * (u64)K;
   // FHE_MODDOWN_FUSED (fused path, K <= 4): the P -> Q conversion runs inside the column-forward
-  // pass of the conversion NTT (k_modup_col, as ModUp), after scaling the P rows into the ext
-  // region (free once the inner product has run): conv is never written in coefficient form.
-  if (fused && FHE_MODDOWN_FUSED && K <= 4 && (u64)c->dnum * rows >= 2 * (u64)K) {
-    u64* ydn = ext;  // [2 batch][K][N]
-    k_modup_scale<<<dim3((u32)(n / kThreads), K, 2 * batch), kThreads, 0, s>>>(
-        accp, rn, L, ydn, K, c->log_n, c->d_moddown_inv, c->d_mods);
-    FHE_HIP_CHECK(hipGetLastError());
+  // pass of the conversion NTT (k_modup_col, as ModUp), on the P rows the INTT has already scaled
+  // into the ext region (free once the inner product has run): conv is never written in
+  // coefficient form.
+  if (fused_down) {
+    // the INTT writes y = [x_k (P^_k)^-1]_{p_k} straight into [2 batch][K][N] (its last stage
+    // folds N^-1 (P^_k)^-1, c->d_nfold_down): no separate scaling pass
+    u64* ydn = ext;
+    if ((rc = launch_ntt_strided(c, false, accp, rn, ydn, (u64)K * n, 2 * batch, L, K, s,
+                                 c->d_nfold_down)))
+      return rc;
     prof_mark(s, "ks_moddown_conv");
     const ModUpColArgs md{ydn, conv, (u64)nlimbs * n, K, nlimbs, nlimbs, 0, nlimbs, limb0, 0,
                           2 * batch, c->d_moddown_hat, M};
@@ -422,6 +434,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
     prof_mark(s, "moddown_row_finish");
     return kOk;
   }
+  if ((rc = launch_ntt(c, false, accp, accp, 2 * batch, rn, L, K, s))) return rc;
   const BcArgs down{accp, rn, L, conv, (u64)nlimbs * n, nlimbs, RowMap{nlimbs, limb0, 0}, 0, 0,
                     2 * batch};
   if ((rc = baseconv_any(K, down, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, s)))
