@@ -161,6 +161,11 @@ struct Layout {
   }
 };
 
+// FHE_FINAL_TOPBITS: the final forward reduction's one-step estimate for moduli just below 2^60
+// (round_compute).
+#ifndef FHE_FINAL_TOPBITS
+#define FHE_FINAL_TOPBITS 1
+#endif
 // kFinalFwd reduces the last forward stage to [0, q); kFinalFwd2 only to [0, 2q) (the fused
 // HomMult tensor: its Montgomery products accept operands below 2q).
 enum Final : int { kNotFinal = 0, kFinalFwd = 1, kFinalInv = 2, kFinalFwd2 = 3 };
@@ -389,12 +394,24 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       // from below r_out q down to [0, q) (kFinalFwd) or [0, 2q) (kFinalFwd2) by halving steps
       constexpr int rout = fwd_range(RIN, KB, H);
       constexpr int stop = FIN == kFinalFwd ? 1 : 2;
+      // q in [2^60 - 2^56, 2^60) (wave-uniform test; the default moduli are the largest primes
+      // below 2^60): x - (x >> 60) q < 2q for any x < 16 q, one estimate instead of up to three
+      // halving steps (k = x >> 60 <= x / q, and x - k q < x (2^60 - q) / 2^60 + q < 2q)
+      if (FHE_FINAL_TOPBITS && rout > 4 && rout <= 16 && (q >> 56) == 15) {
+        const u64 nq = 0 - q;
 #pragma unroll
-      for (int j = 0; j < E; ++j) {
-        static_for<0, 5>([&](auto ci) {
-          constexpr int c = 16 >> decltype(ci)::value;  // 16, 8, 4, 2, 1
-          if constexpr (c >= stop && c < rout) x[j] = csubk(x[j], (u64)c * q);
-        });
+        for (int j = 0; j < E; ++j) {
+          x[j] += (u64)(u32)(x[j] >> 60) * nq;  // x - k q (mod 2^64, exact: the result is >= 0)
+          if constexpr (FIN == kFinalFwd) x[j] = csubk(x[j], q);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          static_for<0, 5>([&](auto ci) {
+            constexpr int c = 16 >> decltype(ci)::value;  // 16, 8, 4, 2, 1
+            if constexpr (c >= stop && c < rout) x[j] = csubk(x[j], (u64)c * q);
+          });
+        }
       }
     }
 #else

@@ -138,3 +138,26 @@ def test_folded_ct_butterfly(q, H):
         o2 = ((u << 1) + 3 * q - s) & M64
         assert o2 == u - v + 3 * q and o2 < H * q
         assert (s - (x + w * y)) % q == 0 and (o2 - (x - w * y)) % q == 0
+
+
+def final_top_bits(x, q):
+    """ntt.hip round_compute, final forward reduction for q in [2^60 - 2^56, 2^60):
+    x + (x >> 60) (-q) mod 2^64."""
+    return (x + (x >> 60) * ((-q) & M64)) & M64
+
+
+@pytest.mark.parametrize("q", [q for q in pyoracle.gen_moduli(16, 20) + pyoracle.gen_moduli(17, 32)
+                               + [(1 << 60) - (1 << 56) + 1] if (q >> 56) == 15])
+def test_final_reduction_by_top_bits(q):
+    """Every x below 16 q (the largest lazy forward range when all q < 2^60) lands in [0, 2q),
+    congruent mod q -- including the worst cases just below multiples of q and 2^60."""
+    rng = random.Random(q)
+    xs = [0, q - 1, q, 2 * q - 1, 16 * q - 1, (1 << 60) - 1, 1 << 60, (15 << 60) - 1, 15 << 60]
+    xs += [k * q - 1 for k in range(1, 17)] + [k << 60 for k in range(1, 16) if (k << 60) < 16 * q]
+    xs += [rng.randrange(16 * q) for _ in range(5000)]
+    for x in xs:
+        if x >= 16 * q:
+            continue
+        r = final_top_bits(x, q)
+        assert 0 <= r < 2 * q, x
+        assert r % q == x % q, x
