@@ -11,6 +11,16 @@ vec_{add,sub,mul}: outputs of the reference itself (/root/reference/arithmetic.p
     (a - b and a * b wrap mod 2^64 before the % there).
 poly_add:  the reference's ' polynomial.py':3-5 called on a 2-component ciphertext; it returns
     None (recorded as ref_returns_none).
+hommult_*: ct x ct HomMult outputs (d0 = a0 b0, d1 = a0 b1 + a1 b0, d2 = a1 b1 in
+    Z_q[X]/(X^N + 1), SURVEY.md §8a') computed ONLY with the reference's own exact vec_mul /
+    vec_add / vec_sub (arithmetic.py:3-13) on dtype=object arrays: the schoolbook negacyclic
+    product is a sum over offsets i of vec_mul(a_i, X^i b), where X^i b is b shifted by i with the
+    wrapped coefficients negated by vec_sub(0, .).  The coefficient-form ring product does not
+    depend on the NTT's psi or output ordering, so this pins the headline HomMult to the
+    reference's arithmetic (the reference's NTT itself is the identity).  Shapes: N = 4096, L = 2
+    on the N = 2^12 chain and N = 2048, L = 8 on the BASELINE configs[2] chain (the 8 largest
+    60-bit primes = 1 mod 2^17, valid NTT primes for any N <= 2^16).
+vec_N65536_L8: vec_* on the configs[2] modulus chain, 4096 coefficients per limb.
 ntt_N4096_L1: the O(N^2) defining sum of SURVEY.md §8a' evaluated in Python big ints (the
     reference's NTT is the identity, arithmetic.py:15-16, so it cannot pin this).
 """
@@ -59,6 +69,56 @@ def vec_fixture(arith, poly, log_n, L, seed, keep_u64):
     return out
 
 
+def ref_negacyclic(arith, a, b, mod_col):
+    """a * b mod (X^N + 1, q_l) per limb row, using only the reference's vec_* (object dtype)."""
+    L, n = a.shape
+    zeros = np.zeros((L, n), dtype=object)
+    acc = zeros.copy()
+    for i in range(n):
+        xb = np.roll(b, i, axis=1)  # X^i b: coefficient k - i moves to k ...
+        if i:
+            xb[:, :i] = arith.vec_sub(zeros[:, :i], xb[:, :i], mod_col)  # ... X^N = -1 on the wrap
+        ai = np.repeat(a[:, i:i + 1], n, axis=1)
+        acc = arith.vec_add(acc, arith.vec_mul(ai, xb, mod_col), mod_col)
+    return acc
+
+
+def hommult_fixture(arith, log_n, qs, seed):
+    n, L = 1 << log_n, len(qs)
+    rng = np.random.default_rng(seed)
+    a = np.stack([np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in qs]) for _ in range(2)])
+    b = np.stack([np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in qs]) for _ in range(2)])
+    for l, q in enumerate(qs):  # edge values: q - 1 and 0 in the leading coefficients
+        a[0, l, :3] = [q - 1, 0, q - 1]
+        b[1, l, :3] = [q - 1, q - 1, 0]
+    mod_col = np.array(qs, dtype=object).reshape(L, 1)
+    ao, bo = a.astype(object), b.astype(object)
+    d0 = ref_negacyclic(arith, ao[0], bo[0], mod_col)
+    d1 = arith.vec_add(ref_negacyclic(arith, ao[0], bo[1], mod_col),
+                       ref_negacyclic(arith, ao[1], bo[0], mod_col), mod_col)
+    d2 = ref_negacyclic(arith, ao[1], bo[1], mod_col)
+    d = np.stack([d0, d1, d2]).astype(np.uint64)
+    return {"a": a, "b": b, "d": d, "moduli": np.array(qs, dtype=np.uint64), "log_n": np.array(log_n),
+            "seed": np.array(seed), "numpy_version": np.array(np.__version__)}
+
+
+def vec_chain_fixture(arith, qs, cols, seed):
+    """vec_* on given moduli rows (L, cols), reference outputs on object inputs."""
+    L = len(qs)
+    rng = np.random.default_rng(seed)
+    a = np.stack([rng.integers(0, q, cols, dtype=np.uint64) for q in qs])
+    b = np.stack([rng.integers(0, q, cols, dtype=np.uint64) for q in qs])
+    for i, q in enumerate(qs):
+        a[i, :4] = [0, q - 1, q - 1, 5]
+        b[i, :4] = [0, q - 1, 1, 5]
+    mod_col = np.array(qs, dtype=object).reshape(L, 1)
+    out = {"a": a, "b": b, "moduli": np.array(qs, dtype=np.uint64), "seed": np.array(seed),
+           "numpy_version": np.array(np.__version__)}
+    for op in ("add", "sub", "mul"):
+        out[op] = getattr(arith, "vec_" + op)(a.astype(object), b.astype(object), mod_col).astype(np.uint64)
+    return out
+
+
 def ntt_fixture(log_n, seed):
     n = 1 << log_n
     q = pyoracle.gen_moduli(log_n, 1)[0]
@@ -76,6 +136,13 @@ def main():
     np.savez(os.path.join(HERE, "vec_N4096_L1.npz"), **vec_fixture(arith, poly, 12, 1, 11, True))
     np.savez(os.path.join(HERE, "vec_N16384_L4.npz"), **vec_fixture(arith, poly, 14, 4, 12, False))
     np.savez(os.path.join(HERE, "ntt_N4096_L1.npz"), **ntt_fixture(12, 13))
+    chain16 = pyoracle.gen_moduli(16, 8)  # BASELINE configs[2] chain (SURVEY.md §8a')
+    np.savez(os.path.join(HERE, "vec_N65536_L8.npz"), **vec_chain_fixture(arith, chain16, 4096, 14))
+    if "--skip-hommult" not in sys.argv:
+        np.savez(os.path.join(HERE, "hommult_N4096_L2.npz"),
+                 **hommult_fixture(arith, 12, pyoracle.gen_moduli(12, 2), 15))
+        np.savez(os.path.join(HERE, "hommult_N2048_L8_chain16.npz"),
+                 **hommult_fixture(arith, 11, chain16, 16))
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))
 
 

@@ -173,6 +173,43 @@ def test_reference_shim_ntt_and_poly_add(fc):
 
 # ------------------------------------------------------------------------------- HomMult
 
+@pytest.mark.parametrize("fx", ["hommult_N4096_L2.npz", "hommult_N2048_L8_chain16.npz"])
+def test_hommult_reference_composed_golden(fc, fx):
+    """HomMult vs the reference's own arithmetic: (d0, d1, d2) in the fixture are schoolbook
+    negacyclic products built only from /root/reference/arithmetic.py:3-13 (vec_mul / vec_add /
+    vec_sub on exact object arrays; tests/golden/make_golden.py).  The N = 2048 case runs on the
+    8-limb BASELINE configs[2] modulus chain."""
+    d = np.load(os.path.join(GOLDEN, fx))
+    log_n = int(d["log_n"])
+    ctx = fc.Context(log_n, moduli=[int(q) for q in d["moduli"]])
+    a = np.stack([d["a"], d["b"][::-1]])  # two ciphertext pairs: (a, b) and (a, b swapped)
+    b = np.stack([d["b"], d["a"][::-1]])
+    got = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    assert (got[0] == d["d"]).all()
+    # second pair: (b1, b0) x (a1, a0) -> d0' = b1 a1 = d2, d1' = b1 a0 + b0 a1 = d1, d2' = d0
+    assert (got[1] == d["d"][::-1]).all()
+
+
+@pytest.mark.parametrize("op", ["add", "sub", "mul"])
+def test_vec_config3_chain_golden(fc, op):
+    """vec_* on the configs[2] chain: the first 4096 coefficients of each N = 2^16 limb are the
+    reference's golden vectors, through the context kernel (k_vec_ctx) and the reference-shaped
+    shim (fhe_vec_op_mod)."""
+    import arithmetic
+
+    d = np.load(os.path.join(GOLDEN, "vec_N65536_L8.npz"))
+    ctx = ctx_for(fc, 16, 8)
+    assert [int(q) for q in d["moduli"]] == ctx.moduli
+    a = rand(ctx.moduli, 16, (1,), seed=31)
+    b = rand(ctx.moduli, 16, (1,), seed=32)
+    a[0, :, :4096], b[0, :, :4096] = d["a"], d["b"]
+    got = fc.to_host(ctx.vec(op, fc.to_device(a), fc.to_device(b)))
+    assert (got[0, :, :4096] == d[op]).all()
+    assert (got == coracle.vec_op(op, a, b, ctx.moduli)).all()
+    shim = getattr(arithmetic, "vec_" + op)(d["a"], d["b"], d["moduli"].reshape(-1, 1))
+    assert (shim == d[op]).all()
+
+
 def test_hommult_config3_matches_oracle(fc):
     ctx = ctx_for(fc, 16, 8)
     a = rand(ctx.moduli, 16, (2, 2), seed=21)

@@ -35,6 +35,25 @@ def test_oracles_match_reference_golden(fx, op):
     assert (c == want).all()
 
 
+@pytest.mark.parametrize("op", ["add", "sub", "mul"])
+def test_oracles_match_reference_golden_config3_chain(op):
+    """vec_* on the BASELINE configs[2] modulus chain (N = 2^16, 8 limbs), reference outputs."""
+    d = _load("vec_N65536_L8.npz")
+    assert [int(q) for q in d["moduli"]] == pyoracle.gen_moduli(16, 8)
+    assert (coracle.vec_op(op, d["a"], d["b"], d["moduli"]) == d[op]).all()
+
+
+@pytest.mark.parametrize("fx", ["hommult_N4096_L2.npz", "hommult_N2048_L8_chain16.npz"])
+def test_oracle_hommult_matches_reference_composed_product(fx):
+    """HomMult pinned to the reference: the fixture's (d0, d1, d2) were computed by the reference's
+    own vec_mul / vec_add / vec_sub (arithmetic.py:3-13) as schoolbook negacyclic products
+    (make_golden.py ref_negacyclic).  The oracle's NTT -> tensor -> INTT must reproduce them."""
+    d = _load(fx)
+    mods = [int(q) for q in d["moduli"]]
+    a, b = d["a"][None], d["b"][None]
+    assert (coracle.hommult(a, b, mods)[0] == d["d"]).all()
+
+
 def test_reference_uint64_divergence_is_recorded():
     """The reference's uint64 path is wrong for sub (a<b) and mul (wraps): the build targets exact
     semantics; the fixture keeps the reference's uint64 outputs to document the divergence."""
