@@ -152,10 +152,12 @@ ModParams make_mod_params(u64 q) {
   ModParams m{};
   m.q = q;
   const u32 bl = 64 - __builtin_clzll(q);
-  if (bl > 61) return m;  // wide modulus: mu = 0 marks the slow exact path
-  m.sh_a = bl - 1;
-  m.sh_b = bl + 3;
-  m.mu = (u64)(((u128)1 << (2 * bl + 2)) / q);
+  // wide modulus (q >= 2^61): mu = 0 marks the exact paths (reduce128_wide, non-lazy butterflies)
+  if (bl <= 61) {
+    m.sh_a = bl - 1;
+    m.sh_b = bl + 3;
+    m.mu = (u64)(((u128)1 << (2 * bl + 2)) / q);
+  }
   if (q & 1) {
     u64 inv = q;  // Newton: each step doubles the correct low bits (q * q = 1 mod 8)
     for (int i = 0; i < 5; ++i) inv *= 2 - q * inv;
@@ -168,7 +170,7 @@ ModParams make_mod_params(u64 q) {
 }
 
 int gen_moduli(u32 log_n, u32 count, u32 bits, u32 skip, u64* out) {
-  if (bits < log_n + 3 || bits > 62) {
+  if (bits < log_n + 3 || bits > 63) {
     set_error("gen_moduli: bits out of range");
     return kInvalid;
   }
@@ -210,9 +212,9 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
   if (K) mods.insert(mods.end(), p, p + K);
   for (size_t i = 0; i < mods.size(); ++i) {
     const u64 m = mods[i];
-    if (m >= (1ull << 61) || m % (2 * n) != 1 || !is_prime_u64(m)) {
+    if (m >= (1ull << 63) || m % (2 * n) != 1 || !is_prime_u64(m)) {
       set_error("ctx_create: modulus #" + std::to_string(i) + " = " + std::to_string(m) +
-                " is not a prime < 2^61 with q = 1 mod 2N");
+                " is not a prime < 2^63 with q = 1 mod 2N");
       return kInvalid;
     }
     for (size_t j = 0; j < i; ++j)
@@ -235,7 +237,11 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
   c->device = device;
   c->num_cus = cus;
   c->lz16 = true;
-  for (u64 m : mods) c->lz16 = c->lz16 && m < (1ull << 60);
+  c->wide = false;
+  for (u64 m : mods) {
+    c->lz16 = c->lz16 && m < (1ull << 60);
+    c->wide = c->wide || m >= (1ull << 61);
+  }
   c->log_n = log_n;
   c->n = n;
   c->L = L;

@@ -19,8 +19,10 @@ constexpr int kThreads = 256;
 
 __device__ __forceinline__ u32 brv(u32 x, u32 bits) { return __builtin_bitreverse32(x) >> (32 - bits); }
 
-// t < 2^64 -> t mod q, any q < 2^61 (Shoup by 1: [0, 3q), then two subtractions)
+// t < 2^64 -> t mod q (Shoup by 1: [0, 3q), then two subtractions; wide moduli 2^61 <= q < 2^63:
+// the exact quotient, [0, 2q), one subtraction)
 __device__ __forceinline__ u64 reduce_word(u64 t, const ModParams& m) {
+  if (m.mu == 0) return csub(shoup_lazy(t, 1, m.ones, m.q), m.q);
   u64 r = shoup_q3(t, 1, m.ones, 0 - m.q);
   r = csub(r, 2 * m.q);
   return csub(r, m.q);

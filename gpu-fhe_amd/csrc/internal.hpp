@@ -32,6 +32,9 @@ struct fhe_ctx {
   int device = 0;
   int num_cus = 0;  // compute units of `device` (one-generation grids of the item-loop kernels)
   bool lz16 = false;  // every modulus < 2^60: forward NTTs may run lazy up to 16q (ntt.hip)
+  // some modulus in [2^61, 2^63): exact (non-lazy) butterflies, HD = 2 in ntt.hip, and the
+  // unfused key-switch (rns.hip)
+  bool wide = false;
   uint32_t log_n = 0;
   uint64_t n = 0;
   uint32_t L = 0, K = 0, dnum = 0, alpha = 0;

@@ -7,7 +7,9 @@
 // so every routine here is written to minimise the number of 32x32 partial products.
 //
 // Conventions (shared with oracle/fhe_oracle.c):
-//  * moduli q < 2^61, so lazy values in [0, 4q) fit a word with room to spare;
+//  * context moduli q < 2^63.  "Narrow" moduli (q < 2^61, Barrett constants present, mu != 0)
+//    take the lazy butterflies and Montgomery / 128-bit-sum shortcuts; "wide" ones
+//    (2^61 <= q < 2^63, mu == 0) the exact forms below (values kept below 2q < 2^64);
 //  * Shoup: w' = floor(w * 2^64 / q) precomputed for a constant operand w;
 //  * Barrett (data x data): z < 4q^2, a = bitlen(q) - 1, b = 2 bitlen(q) + 2,
 //    mu = floor(2^b / q); estimate floor(floor(z / 2^a) * mu / 2^(b - a)) is at most 2 low,
@@ -146,8 +148,19 @@ __device__ __forceinline__ u64 sub_plus(u64 a, u64 b, u64 kp1) {
   return (a + kp1) + nb;
 }
 
-// Barrett reduction of a 128-bit z < 4 q^2 into [0, q).
+// Full reduction of a 128-bit z = (zhi, zlo) into [0, q) for a wide modulus 2^61 <= q < 2^63
+// (also valid below): zhi 2^64 + zlo = zhi (2^64 mod q) + zlo, each term by an exact-quotient
+// Shoup product into [0, 2q) (2q < 2^64), then three conditional subtractions.
+__device__ __forceinline__ u64 reduce128_wide(u64 zlo, u64 zhi, const ModParams& m) {
+  const u64 q = m.q;
+  const u64 a = csub(shoup_lazy(zhi, m.r64, m.r64s, q), q);
+  const u64 b = csub(shoup_lazy(zlo, 1, m.ones, q), q);
+  return csub(a + b, q);
+}
+
+// Barrett reduction of a 128-bit z < 4 q^2 into [0, q) (wide moduli: reduce128_wide).
 __device__ __forceinline__ u64 barrett_reduce(u128 z, const ModParams& m) {
+  if (m.mu == 0) return reduce128_wide((u64)z, (u64)(z >> 64), m);
   const u64 z1 = (u64)(z >> m.sh_a);
   const u64 est = (u64)(((u128)z1 * m.mu) >> m.sh_b);
   u64 r = (u64)z - est * m.q;
@@ -208,6 +221,11 @@ __device__ __forceinline__ u64 reduce128(u64 zlo, u64 zhi, const ModParams& m) {
   return csub(r, m.q);
 }
 
+// reduce128 for any context modulus (wide ones by reduce128_wide; a wave-uniform branch when m is).
+__device__ __forceinline__ u64 reduce128_any(u64 zlo, u64 zhi, const ModParams& m) {
+  return m.mu == 0 ? reduce128_wide(zlo, zhi, m) : reduce128(zlo, zhi, m);
+}
+
 // Full reduction of any 64-bit x into [0, q), any q >= 2: Barrett for 2^31 <= q < 2^61
 // (x < 2^64 <= 4 q^2 there), repeated subtraction above (x < 8q), hardware % below.
 __device__ __forceinline__ u64 reduce_u64(u64 x, const ModParams& m) {
@@ -220,9 +238,10 @@ __device__ __forceinline__ u64 reduce_u64(u64 x, const ModParams& m) {
 }
 
 // Exact a * b mod q for a, b < q and any q < 2^64 (generic entry points only; the context
-// kernels use Shoup/Barrett).  Wide moduli fall back to a 64-step double-and-add.
+// kernels use Shoup/Barrett).  q < 2^63: Barrett / reduce128_wide; above, a 64-step
+// double-and-add.
 __device__ __forceinline__ u64 mulmod_any(u64 a, u64 b, const ModParams& m) {
-  if (m.mu != 0) return barrett_reduce((u128)a * b, m);
+  if (m.q < (1ull << 63)) return barrett_reduce((u128)a * b, m);
   u64 r = 0;
   for (int i = 63; i >= 0; --i) {
     const u64 r2 = r >= m.q - r ? r - (m.q - r) : r + r;  // 2r mod q without overflow

@@ -355,7 +355,30 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
   [[maybe_unused]] u64 q3 = 3 * q;
   [[maybe_unused]] const u64 q4 = 4 * q;
   asm("" : "+s"(q3));
-  if constexpr (FWD) {
+  if constexpr (FWD && H == 2) {
+    // wide moduli (2^61 <= q < 2^63, ctx->wide): no lazy headroom.  Values stay below 2q:
+    // u = x mod q, v = (w x') mod q by the exact-quotient Shoup product (any 64-bit x', [0, 2q)
+    // then one subtraction), outputs u + v and u - v + q, both in [0, 2q).
+    static_for<0, KB>([&](auto sc) {
+      constexpr int b = KB - 1 - decltype(sc)::value;
+      const int bitpos = LO + b;
+      const int st = LOGR - 1 - bitpos;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        if (j & (1 << b)) continue;
+        const int jj = j | (1 << b);
+        const ulonglong2 w = twiddle(b, j, bitpos, st);
+        const u64 u = csubk(x[j], q);
+        const u64 v = csubk(shoup_fast(x[jj], w.x, w.y, nq), q);
+        x[j] = u + v;
+        x[jj] = u - v + q;
+      }
+    });
+    if constexpr (FIN == kFinalFwd) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) x[j] = csubk(x[j], q);
+    }
+  } else if constexpr (FWD) {
 #if FHE_BFLY == 2
     // CT: X-operands below r q (the static range of this stage, fwd_range), reduced by H/2 q
     // only when the stage would outgrow H q; v = w x[jj] in [0, 3q); outputs below (r' + 3) q
@@ -446,6 +469,28 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       }
     }
 #endif
+  } else if constexpr (H == 2) {
+    // wide GS: canonical inputs; sum mod q, (u - v + q) w by the exact Shoup product, reduced
+    static_for<0, KB>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      constexpr int bitpos = LO + b;
+      constexpr int st = LOGR - 1 - bitpos;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        if (j & (1 << b)) continue;
+        const int jj = j | (1 << b);
+        const u64 u = x[j], v = x[jj];
+        const u64 sum = u + v, dif = u - v + q;
+        if constexpr (FIN == kFinalInv && st == 0) {
+          x[j] = csubk(shoup_fast(sum, nf0.x, nf0.y, nq), q);
+          x[jj] = csubk(shoup_fast(dif, nf1.x, nf1.y, nq), q);
+        } else {
+          const ulonglong2 w = twiddle(b, j, bitpos, st);
+          x[j] = csubk(sum, q);
+          x[jj] = csubk(shoup_fast(dif, w.x, w.y, nq), q);
+        }
+      }
+    });
   } else {
 #pragma unroll
     for (int b = 0; b < KB; ++b) {
@@ -965,7 +1010,8 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
     constexpr int k = decltype(kc)::value;
     constexpr int KB = Rd::kb(k);
     constexpr int LO = Rd::lo_fwd(k);
-    constexpr int F = (k == Rd::NR - 1) ? kFinalFwd2 : kNotFinal;
+    // wide moduli: canonical forward outputs (4 q^2 would exceed q R for q > 2^62)
+    constexpr int F = (k == Rd::NR - 1) ? (HR == 2 ? kFinalFwd : kFinalFwd2) : kNotFinal;
     constexpr int RIN = fwd_range(fwd_range(1, G::N1, HR), G::N2 - (LO + KB), HR);
     using Lay = Layout<G::N2, KB, LO>;
     const u32 tp = Lay::tpos(t);
@@ -1011,6 +1057,10 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
       v[j] = mont_reduce_lazy((u64)t, (u64)(t >> 64), q, m.qinv);
     }
   }
+  if constexpr (HR == 2) {  // the wide inverse takes canonical inputs
+#pragma unroll
+    for (int j = 0; j < kE; ++j) v[j] = csubk(v[j], q);
+  }
   // inverse row pass: its first round butterflies the low bits, the layout the tensor used
   static_assert(Rd::lo_fwd(Rd::NR - 1) == Rd::lo_inv(0) && Rd::kb(Rd::NR - 1) == Rd::kb_inv(0),
                 "tensor layout must match the first inverse round");
@@ -1024,7 +1074,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
       lds_sync<SY>();
       if (active) own.template load<Lay>(v, tp);
     }
-    if (active) round_compute<G::N2, KB, LO, false, kNotFinal, true>(v, tp, ti, base, q, {0, 0}, {0, 0});
+    if (active) round_compute<G::N2, KB, LO, false, kNotFinal, true, HR>(v, tp, ti, base, q, {0, 0}, {0, 0});
     if constexpr (k == Rd::NR - 1) {
       const GView<1, kHmNT> gout{d + ((u64)b * 3 + grp) * limbN + loc, 0};
       if (active) gout.template store<Lay>(v, tp);
@@ -1332,6 +1382,10 @@ dim3 item_grid(const fhe_ctx* c, int threads, u64 items) {
   return dim3((u32)g);
 }
 
+// The inverse passes' H: the lazy inverse does not depend on the forward headroom (one build for
+// H = 8 and 16); wide contexts (H = 2) take the exact one.
+constexpr int inv_h(int hd) { return hd == 2 ? 2 : 8; }
+
 // Row pass of a standalone NTT over [polys][nlimbs][N] (src poly stride sp -> dst stride dp).
 template <int LOGN, int HD>
 void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 dp, u32 polys,
@@ -1347,8 +1401,8 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
         <<<item_grid<k_ntt_row<LOGN, true, HD, false, OUT>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
            0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, twf, c->d_mods);
   else  // the inverse's first pass
-    k_ntt_row<LOGN, false, 8, IN, false>
-        <<<item_grid<k_ntt_row<LOGN, false, 8, IN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
+    k_ntt_row<LOGN, false, inv_h(HD), IN, false>
+        <<<item_grid<k_ntt_row<LOGN, false, inv_h(HD), IN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
            0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, twi, c->d_mods);
 }
 
@@ -1375,8 +1429,8 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   } else {
     row_pass<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_inv");
-    k_ntt_col<LOGN, false, 8, false, OUT>
-        <<<item_grid<k_ntt_col<LOGN, false, 8, false, OUT>, false>(c, G::THR_C, ic),
+    k_ntt_col<LOGN, false, inv_h(HD), false, OUT>
+        <<<item_grid<k_ntt_col<LOGN, false, inv_h(HD), false, OUT>, false>(c, G::THR_C, ic),
            G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv,
                              nfold ? nfold : c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_inv");
@@ -1407,8 +1461,8 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   prof_mark(s, "hm_row_tensor");
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
-  k_ntt_col<LOGN, false, 8, kHmNT, kHmNT>
-      <<<item_grid<k_ntt_col<LOGN, false, 8, kHmNT, kHmNT>, false>(c, G::THR_C, ii),
+  k_ntt_col<LOGN, false, inv_h(HD), kHmNT, kHmNT>
+      <<<item_grid<k_ntt_col<LOGN, false, inv_h(HD), kHmNT, kHmNT>, false>(c, G::THR_C, ii),
          G::THR_C, 0, s>>>(d, nullptr, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv,
                            c->d_nfold + 2, c->d_mods);
   prof_mark(s, "hm_col_inv");
@@ -1424,6 +1478,12 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
 #if FHE_NTT_KS_ONLY
 
 namespace {
+// The fused key-switch kernels rely on lazy ranges and 128-bit sums that need q < 2^61; wide
+// contexts take the unfused key-switch (rns.hip), which never calls these launchers.
+int wide_unsupported() {
+  set_error("fused key-switch kernels need every modulus < 2^61");
+  return kUnsupported;
+}
 template <int LOGN, int HD>
 void col_fwd_pass(const fhe_ctx* c, const u64* src, u64 sp, u64* dst, u64 dp, u32 polys,
                   u32 limb0, u32 nlimbs, hipStream_t s) {
@@ -1460,6 +1520,7 @@ int ks_row_inner_dispatch(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
 int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
                        u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
   if ((u64)polys * nlimbs == 0) return kOk;
+  if (c->wide) return wide_unsupported();
   switch (c->log_n) {
 #define X(n)                                                                                 \
   case n:                                                                                    \
@@ -1501,6 +1562,7 @@ int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
 
 int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
   if ((u64)a.T * a.batch == 0) return kOk;
+  if (c->wide) return wide_unsupported();
   switch (c->log_n) {
 #define X(n) \
   case n:    \
@@ -1525,6 +1587,7 @@ void moddown_row_dispatch(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t
 
 int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s) {
   if ((u64)a.batch * a.nq == 0) return kOk;
+  if (c->wide) return wide_unsupported();
   switch (c->log_n) {
 #define X(n)                                                                                   \
   case n:                                                                                      \
@@ -1543,6 +1606,7 @@ int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s)
 
 int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
   if ((u64)a.rows * a.batch == 0) return kOk;
+  if (c->wide) return wide_unsupported();
   switch (c->log_n) {
 #define X(n) \
   case n:    \
@@ -1568,10 +1632,12 @@ int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstr
   switch (c->log_n) {
 #define X(n) \
   case n:    \
-    return c->lz16 ? ntt_dispatch<n, 16>(c, forward, src, spstride, dst, dpstride, polys, limb0, \
-                                         nlimbs, s, nfold)                                     \
-                   : ntt_dispatch<n, 8>(c, forward, src, spstride, dst, dpstride, polys, limb0,  \
-                                        nlimbs, s, nfold);
+    return c->wide   ? ntt_dispatch<n, 2>(c, forward, src, spstride, dst, dpstride, polys, limb0, \
+                                          nlimbs, s, nfold)                                     \
+           : c->lz16 ? ntt_dispatch<n, 16>(c, forward, src, spstride, dst, dpstride, polys, limb0, \
+                                           nlimbs, s, nfold)                                    \
+                     : ntt_dispatch<n, 8>(c, forward, src, spstride, dst, dpstride, polys, limb0,  \
+                                          nlimbs, s, nfold);
     FHE_LOGN_CASES(X)
 #undef X
   }
@@ -1588,8 +1654,9 @@ static int hommult_chunk(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u
   switch (c->log_n) {
 #define X(n) \
   case n:    \
-    return c->lz16 ? hommult_dispatch<n, 16>(c, d, a, b, batch, limb0, nlimbs, x, s) \
-                   : hommult_dispatch<n, 8>(c, d, a, b, batch, limb0, nlimbs, x, s);
+    return c->wide   ? hommult_dispatch<n, 2>(c, d, a, b, batch, limb0, nlimbs, x, s)  \
+           : c->lz16 ? hommult_dispatch<n, 16>(c, d, a, b, batch, limb0, nlimbs, x, s) \
+                     : hommult_dispatch<n, 8>(c, d, a, b, batch, limb0, nlimbs, x, s);
     FHE_LOGN_CASES(X)
 #undef X
   }

@@ -33,9 +33,9 @@ __global__ __launch_bounds__(kThreads) void k_tensor_ntt(u64* __restrict__ d,
   const u128 t0 = (u128)a0 * b0, t2 = (u128)a1 * b1;
   const u128 t1 = (u128)a0 * b1 + (u128)a1 * b0;
   u64* o = d + bt * 3 * ln + (u64)l * n + c;
-  o[0] = reduce128((u64)t0, (u64)(t0 >> 64), m);
-  o[ln] = reduce128((u64)t1, (u64)(t1 >> 64), m);
-  o[2 * ln] = reduce128((u64)t2, (u64)(t2 >> 64), m);
+  o[0] = reduce128_any((u64)t0, (u64)(t0 >> 64), m);
+  o[ln] = reduce128_any((u64)t1, (u64)(t1 >> 64), m);
+  o[2 * ln] = reduce128_any((u64)t2, (u64)(t2 >> 64), m);
 }
 
 // out[b][0] = d[b][0] + ks0[b], out[b][1] = d[b][1] + ks1[b] (mod q).

@@ -51,8 +51,10 @@ inline ulonglong2 shoup_pair(u64 w, u64 q) {
 // on a scalar load per row; each output is a 128-bit sum of S full products y_k * (S^_k mod t)
 // (< S t^2 < 2^126), reduced once (Montgomery for S < 8, else reduce128), instead of S Shoup
 // products and S subtractions.
+// WIDE (contexts with a modulus >= 2^61): the products' sum could pass 2^128, so each product
+// y_k (S^_k mod t) is reduced on its own (reduce128_wide) and the sum kept below t.
 constexpr int kMaxRows = 64;
-template <int S>
+template <int S, bool WIDE>
 __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ in, u64 in_bs,
                                                        u32 src0, u64* __restrict__ out, u64 out_bs,
                                                        u32 T, RowMap map, u32 skip_lo, u32 skip_hi,
@@ -61,9 +63,9 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
                                                        const ModParams* __restrict__ mods) {
   // S < 8: y_k < 2^61 and S 2^61 < 2^64, so the sum stays below t 2^64 and one Montgomery
   // reduction (R = 2^64, folded into the table's second word) replaces reduce128
-  constexpr bool kMont = S < 8;
+  constexpr bool kMont = !WIDE && S < 8;
   // S <= 4: the sums run on 30-bit pieces (Sum30), the LDS holding split30(hat)
-  constexpr bool kSplit = S <= 4;
+  constexpr bool kSplit = !WIDE && S <= 4;
   __shared__ u64 s_hat[kMaxRows * S];
   __shared__ u32 s_limb[kMaxRows];
   for (u32 e = threadIdx.x; e < T * S; e += blockDim.x) {
@@ -94,6 +96,17 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
       for (int k = 0; k < S; ++k) acc.add(y[k], s_hat[r * S + k]);
       const ModParams& m = mods[limb];
       out[(u64)r * n + i] = acc.mont(m.q, m.qinv);
+      continue;
+    }
+    if constexpr (WIDE) {
+      const ModParams& m = mods[limb];
+      u64 sum = 0;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const u128 p = (u128)y[k] * s_hat[r * S + k];
+        sum = csub(sum + reduce128_wide((u64)p, (u64)(p >> 64), m), m.q);
+      }
+      out[(u64)r * n + i] = sum;
       continue;
     }
     u128 acc = 0;
@@ -136,6 +149,22 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc, u6
   for (int j = 0; j < DNUM; ++j) {
     kb[j] = evk_b[(u64)j * rn + e];
     ka[j] = evk_a[(u64)j * rn + e];
+  }
+  if (m.mu == 0) {  // wide modulus (uniform): DNUM products could pass 2^128, reduce each
+    for (u32 b = 0; b < batch; ++b) {
+      u64 s0 = 0, s1 = 0;
+#pragma unroll
+      for (int j = 0; j < DNUM; ++j) {
+        const u64 x = (u32)j == own ? d2_own[((u64)b * nq + r) * n + i]
+                                    : ext[((u64)j * batch + b) * rn + e];
+        const u128 p0 = (u128)x * kb[j], p1 = (u128)x * ka[j];
+        s0 = csub(s0 + reduce128_wide((u64)p0, (u64)(p0 >> 64), m), m.q);
+        s1 = csub(s1 + reduce128_wide((u64)p1, (u64)(p1 >> 64), m), m.q);
+      }
+      acc[(u64)b * rn + e] = s0;
+      acc[acc_ws + (u64)b * rn + e] = s1;
+    }
+    return;
   }
   for (u32 b = 0; b < batch; ++b) {
     u128 s0 = 0, s1 = 0;
@@ -237,7 +266,7 @@ struct BcArgs {
   u32 batch;
 };
 
-template <int S>
+template <int S, bool WIDE>
 void launch_bc(const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* hat, u32 hs,
                const ModParams* mods, hipStream_t s) {
   const dim3 g((u32)((n + kThreads - 1) / kThreads), a.batch);
@@ -252,17 +281,21 @@ void launch_bc(const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* 
       m.base1 += r0 - m.n0;
       m.n0 = 0;
     }
-    k_baseconv<S><<<g, kThreads, 0, s>>>(a.in, a.in_bs, a.src0, a.out + (u64)r0 * n, a.out_bs, t,
+    k_baseconv<S, WIDE><<<g, kThreads, 0, s>>>(a.in, a.in_bs, a.src0, a.out + (u64)r0 * n, a.out_bs, t,
                                          m, a.skip_lo, a.skip_hi, n, inv, hat, hs, mods);
   }
 }
 
 int baseconv_any(u32 S, const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* hat,
-                 u32 hs, const ModParams* mods, hipStream_t s) {
+                 u32 hs, const ModParams* mods, bool wide, hipStream_t s) {
   switch (S) {
-#define X(k) \
-  case k:    \
-    launch_bc<k>(a, n, inv, hat, hs, mods, s); break;
+#define X(k)                                    \
+  case k:                                       \
+    if (wide)                                   \
+      launch_bc<k, true>(a, n, inv, hat, hs, mods, s); \
+    else                                        \
+      launch_bc<k, false>(a, n, inv, hat, hs, mods, s); \
+    break;
     X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #undef X
     default:
@@ -352,7 +385,9 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   // FHE_KS_FUSED: for dnum <= 4 the digits get only their column-forward pass here, and one fused
   // kernel (ntt.hip, k_ks_row_inner) runs every digit's row-forward pass and the inner product
   // (no NTT-form ext in HBM, no separate inner-product pass); otherwise full NTTs + k_ks_inner.
-  const bool fused = FHE_KS_FUSED && c->dnum <= 4;
+  // Wide contexts (a modulus >= 2^61) take the unfused kernels: the fused ones rely on lazy
+  // ranges and 128-bit sums that need q < 2^61.
+  const bool fused = FHE_KS_FUSED && c->dnum <= 4 && !c->wide;
   // FHE_MODUP_FUSED (with the fused row kernel, digits of <= 4 limbs): the base conversion runs
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
   // digit's source rows; the extended rows are never written in coefficient form.
@@ -383,7 +418,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
     }
     const BcArgs up{c_all + (u64)lo * n, (u64)L * n, lo, e, rn, rows, map, lo, hi, batch};
     if ((rc = baseconv_any(hi - lo, up, n, c->d_modup_inv + (size_t)j * alpha,
-                           c->d_modup_hat + (size_t)j * alpha * M, M, c->d_mods, s)))
+                           c->d_modup_hat + (size_t)j * alpha * M, M, c->d_mods, c->wide, s)))
       return rc;
     // own Q-limbs outside [lo, hi): up to two ranges, then the P-limbs
     const u32 a0 = limb0, a1 = std::min(limb0 + nlimbs, lo);
@@ -437,7 +472,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   if ((rc = launch_ntt(c, false, accp, accp, 2 * batch, rn, L, K, s))) return rc;
   const BcArgs down{accp, rn, L, conv, (u64)nlimbs * n, nlimbs, RowMap{nlimbs, limb0, 0}, 0, 0,
                     2 * batch};
-  if ((rc = baseconv_any(K, down, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, s)))
+  if ((rc = baseconv_any(K, down, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, c->wide, s)))
     return rc;
   prof_mark(s, "ks_moddown_conv");
   if (fused) {  // conversion NTT's row pass finishes ModDown in its epilogue
@@ -474,7 +509,7 @@ int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u3
   FHE_HIP_CHECK(hipMemcpyAsync(d_tab + inv.size(), hat.data(), hat.size() * 16,
                                hipMemcpyHostToDevice, s));
   const BcArgs a{in, 0, s0, out, 0, T, RowMap{T, t0, 0}, 0, 0, 1};
-  const int rc = baseconv_any(S, a, c->n, d_tab, d_tab + inv.size(), M, c->d_mods, s);
+  const int rc = baseconv_any(S, a, c->n, d_tab, d_tab + inv.size(), M, c->d_mods, c->wide, s);
   // the host vectors must outlive the async copies
   FHE_HIP_CHECK(hipStreamSynchronize(s));
   FHE_HIP_CHECK(hipFreeAsync(d_tab, s));

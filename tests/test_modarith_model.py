@@ -161,3 +161,93 @@ def test_final_reduction_by_top_bits(q):
         r = final_top_bits(x, q)
         assert 0 <= r < 2 * q, x
         assert r % q == x % q, x
+
+
+# ---- wide moduli (2^61 <= q < 2^63): exact (non-lazy) forms, ntt.hip H = 2 ------------------
+
+def shoup_fast(y, w, ws, q):
+    """modarith.hpp shoup_fast: exact quotient h = floor(y ws / 2^64), remainder lo64(y w + h nq)
+    by the 6-mad chain (low words through the chain's carries, cross terms into the high word)."""
+    y0, y1 = y & M32, y >> 32
+    s0, s1 = ws & M32, ws >> 32
+    w0, w1 = w & M32, w >> 32
+    nq = (-q) & M64
+    n0, n1 = nq & M32, nq >> 32
+    a = y1 * s0 + ((y0 * s0) >> 32)
+    b = y0 * s1 + (a & M32)
+    h = (y1 * s1 + (a >> 32) + (b >> 32)) & M64
+    h0, h1 = h & M32, h >> 32
+    t = (h0 * n0 + y0 * w0) & M64
+    c = (y1 * w0 + (t >> 32)) & M64
+    c = (y0 * w1 + c) & M64
+    c = (h1 * n0 + c) & M64
+    c = (h0 * n1 + c) & M64
+    return ((c & M32) << 32) | (t & M32)
+
+
+def reduce128_wide(z, q):
+    """modarith.hpp reduce128_wide: zhi (2^64 mod q) + zlo, each by an exact Shoup product."""
+    r64 = (1 << 64) % q
+    a = shoup_fast(z >> 64, r64, (r64 << 64) // q, q)
+    a = a - q if a >= q else a
+    b = shoup_fast(z & M64, 1, (1 << 64) // q, q)
+    b = b - q if b >= q else b
+    s = a + b
+    return s - q if s >= q else s
+
+
+def _wide_moduli():
+    qs = pyoracle.gen_moduli(12, 2, bits=62) + pyoracle.gen_moduli(12, 2, bits=63)
+    qs += pyoracle.gen_moduli(16, 1, bits=63) + pyoracle.gen_moduli(17, 1, bits=62)
+    qs.append(pyoracle.gen_moduli(10, 1, bits=61)[0])
+    return qs
+
+
+@pytest.mark.parametrize("q", _wide_moduli())
+def test_shoup_fast_exact_range(q):
+    """Exact-quotient Shoup: any 64-bit y lands in [0, 2q) (< 2^64 for q < 2^63), congruent."""
+    rng = random.Random(q + 11)
+    cases = [(y, w) for y in [0, 1, q - 1, 2 * q - 1, M64, 1 << 63] for w in [0, 1, q - 1, q // 2]]
+    cases += [(rng.getrandbits(64), rng.randrange(q)) for _ in range(3000)]
+    for y, w in cases:
+        r = shoup_fast(y, w, (w << 64) // q, q)
+        assert 0 <= r < 2 * q and r % q == (y * w) % q, (y, w)
+
+
+@pytest.mark.parametrize("q", _wide_moduli())
+def test_wide_butterfly_ranges(q):
+    """ntt.hip H = 2: CT inputs below 2q give outputs below 2q; GS keeps canonical values; every
+    csub_fast operand is within 2^63 of its modulus (the sign-mask select's validity)."""
+    rng = random.Random(q + 12)
+    for _ in range(3000):
+        w = rng.randrange(q)
+        ws = (w << 64) // q
+        x, y = rng.randrange(2 * q), rng.randrange(1 << 64)
+        u = csub_fast(x, q)
+        v = csub_fast(shoup_fast(y, w, ws, q), q)
+        assert u < q and v < q
+        a, b = u + v, u - v + q
+        assert a < 2 * q and 0 < b < 2 * q and 2 * q < 1 << 64
+        assert (a - (x + w * y)) % q == 0 and (b - (x - w * y)) % q == 0
+        x, y = rng.randrange(q), rng.randrange(q)
+        s = csub_fast(x + y, q)
+        d = csub_fast(shoup_fast(x - y + q, w, ws, q), q)
+        assert s == (x + y) % q and d == ((x - y) * w) % q
+
+
+@pytest.mark.parametrize("q", _wide_moduli())
+def test_reduce128_wide_and_wide_tensor(q):
+    """reduce128_wide on every 128-bit value; the fused HomMult's Montgomery tensor on canonical
+    operands (wide contexts reduce the forward output to [0, q): d1 < 2 q^2 < q 2^64)."""
+    rng = random.Random(q + 13)
+    zs = [0, 1, (1 << 128) - 1, q * q - 1, (q - 1) << 64]
+    zs += [rng.getrandbits(128) for _ in range(3000)]
+    for z in zs:
+        assert reduce128_wide(z, q) == z % q, z
+    R_inv = pow(1 << 64, -1, q)
+    for _ in range(2000):
+        a0, a1, b0, b1 = (rng.randrange(q) for _ in range(4))
+        t = a0 * b1 + a1 * b0
+        assert t < q << 64
+        r = mont_reduce_lazy(t, q)
+        assert 0 <= r < 2 * q and r % q == (t * R_inv) % q
