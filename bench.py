@@ -53,6 +53,9 @@ def parse():
                     help="ciphertexts per GPU per step (default 64 for hommult -- the throughput "
                          "batch: +3.5 %% over 16, fewer launch tails -- and 16 for the others)")
     ap.add_argument("--log-n", type=int, default=16)
+    ap.add_argument("--bits", type=int, default=60, choices=[60, 61, 62, 63],
+                    help="hommult: modulus chain of the largest primes below 2^bits (62, 63: the "
+                         "exact wide-modulus butterflies)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -161,11 +164,57 @@ def roofline(kernel, alg_bytes, ms, shape):
             "kernel": kernel, "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(ms, 4)}
 
 
+_PEAKS = {}
+
+
+def alu_peaks():
+    """Butterflies/s ceilings of the NTT arithmetic on this GPU (tools/microbench/bfly_peak.hip:
+    the kernels' exact forward CT / inverse GS instruction sequences, register-resident, full
+    occupancy, no memory traffic), measured once per process on the warmed-up chip."""
+    if not _PEAKS:
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "microbench", "libbflypeak.so"))
+        lib.fhe_peak_bfly.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double)]
+        blocks = 8 * torch.cuda.get_device_properties(0).multi_processor_count
+        for inv in (0, 1):
+            rate, ms = ctypes.c_double(), ctypes.c_double()
+            if lib.fhe_peak_bfly(inv, blocks, 256, 20, ctypes.byref(rate), ctypes.byref(ms)):
+                raise RuntimeError("fhe_peak_bfly failed")
+            _PEAKS["inv" if inv else "fwd"] = rate.value
+    return _PEAKS
+
+
+def row_bflies(log_n):
+    """Butterflies in one row pass of one poly-limb (the last log R2 stages of N = R1 x R2)."""
+    return (1 << log_n) // 2 * (log_n - log_n // 2)
+
+
+def roofline_alu(kernel, fwd_bflies, inv_bflies, ms, valu_per_bfly=None):
+    """Integer-ALU roofline of a launch that runs `fwd_bflies` forward and `inv_bflies` inverse
+    butterflies in `ms`: the ceiling time at the measured butterfly rates vs the measured time."""
+    pk = alu_peaks()
+    t_ceil = fwd_bflies / pk["fwd"] + inv_bflies / pk["inv"]
+    total = fwd_bflies + inv_bflies
+    achieved = total / (ms * 1e-3) / 1e12
+    peak = total / t_ceil / 1e12
+    out = {"bound": "valu", "achieved": round(achieved, 4), "peak": round(peak, 4),
+           "unit": "Tbutterfly/s", "frac": round(achieved / peak, 4), "kernel": kernel,
+           "butterflies_per_launch": {"forward": fwd_bflies, "inverse": inv_bflies},
+           "peak_source": "tools/microbench/bfly_peak.hip, measured in this run "
+                          f"(forward {pk['fwd'] / 1e12:.3f}, inverse {pk['inv'] / 1e12:.3f} "
+                          "Tbutterfly/s)"}
+    if valu_per_bfly:
+        out["valu_instr_per_butterfly"] = valu_per_bfly
+    return out
+
+
 def run_hommult(args, world, rank):
     L = 8
     shard = fdist.LimbShard(L, world, rank)
     n = 1 << args.log_n
-    ctx = fc.Context(args.log_n, L=L)
+    mods = fc.gen_moduli(args.log_n, L, bits=args.bits) if args.bits != 60 else None
+    ctx = fc.Context(args.log_n, moduli=mods) if mods else fc.Context(args.log_n, L=L)
     gen = torch.Generator(device="cuda")
     gen.manual_seed(1234 + rank)
     gbatch = args.batch * world  # ciphertext pairs per step, whole job
@@ -182,18 +231,17 @@ def run_hommult(args, world, rank):
     dom = "hm_row_tensor"
     alg = gbatch * 7 * shard.nlimbs * n * 8
 
-    # NTT throughput rides along: forward NTTs on this rank's limbs, 64 polys per call
+    # NTT throughput rides along (BASELINE metric "NTTs/sec"): forward + inverse NTTs of 64 polys
+    # on this rank's limbs, sustained (warmed up, then timed like the main leg), every NTT counted
     x = uniform_limbs(gen, mods, (64,), n)
-    nsteps = 10
-    for _ in range(3):
+
+    def ntt_pair():
         ctx.ntt_(x, limb0=shard.lo)
-    barrier(world)
-    t1 = time.perf_counter()
-    for _ in range(nsteps):
-        ctx.ntt_(x, limb0=shard.lo)
-    barrier(world)
-    ntt_dt = max_over_ranks(time.perf_counter() - t1, world)
-    ntt_per_s = 64 * shard.nlimbs * world * nsteps / ntt_dt
+        ctx.intt_(x, limb0=shard.lo)
+
+    nargs = argparse.Namespace(warmup=50, steps=100)
+    ntt_dt, ntt_k = timed(ntt_pair, nargs, world, 8 * nargs.steps + 8)
+    ntt_per_s = 2 * 64 * shard.nlimbs * world * nargs.steps / ntt_dt
     pipe_gbps = hm_per_s * 7 * L * n * 8 / 1e9 / world
     out = {
         "metric": METRIC, "value": round(hm_per_s, 2), "unit": "HomMult/s",
@@ -202,13 +250,31 @@ def run_hommult(args, world, rank):
                    "log_n": args.log_n, "limbs": L, "batch_per_gpu": args.batch,
                    "global_batch": gbatch, "parallelism": f"rns-limb-shard x{world}"},
         "ntt_per_sec": round(ntt_per_s, 1),
-        "ntt_config": {"log_n": args.log_n, "direction": "forward", "polys": 64,
-                       "limbs_per_gpu": shard.nlimbs},
+        "ntt_config": {"log_n": args.log_n, "direction": "forward+inverse", "polys": 64,
+                       "limbs_per_gpu": shard.nlimbs, "warmup": nargs.warmup,
+                       "steps": nargs.steps},
+        "ntt_kernel_ms": {k: round(v, 4) for k, v in ntt_k.items()},
         "hommult_pipeline_hbm_gbps_per_gpu": round(pipe_gbps, 1),
         "hommult_pipeline_frac_of_peak": round(pipe_gbps / HBM_PEAK_GBPS, 4),
         "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
         "roofline": roofline(dom, alg, kavg.get(dom, float("nan")), shape),
     }
+    # the fused row kernel is limited by VALU issue: its integer-ALU roofline, and
+    # the same for the whole pipeline (7 full NTTs per ct x ct limb)
+    units = gbatch * shard.nlimbs
+    rb = row_bflies(args.log_n)
+    if not args.bits > 60:  # the ceiling kernel runs the lazy (q < 2^61) arithmetic
+        out["roofline_alu"] = roofline_alu(dom, 4 * rb * units, 3 * rb * units,
+                                           kavg.get(dom, float("nan")),
+                                           {"forward": 18, "inverse": 21})
+        full = (n // 2) * args.log_n
+        out["hommult_pipeline_alu"] = roofline_alu("hm_col_fwd + hm_row_tensor + hm_col_inv",
+                                                   4 * full * units, 3 * full * units,
+                                                   sum(kavg.values()))
+    out["limiter"] = "valu" if out.get("roofline_alu", {}).get("frac", 0) > \
+        out["roofline"]["frac"] else "hbm"
+    if args.bits != 60:
+        out["config"]["modulus_bits"] = args.bits
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_hommult(ctx.moduli, args.log_n, args.cpu_seconds)
@@ -240,6 +306,13 @@ def run_ntt(args, world, rank):
            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
            # every NTT pass reads and writes each coefficient once
            "roofline": roofline(dom, polys * shard.nlimbs * n * 16, kavg[dom], shape)}
+    # butterflies of the dominant pass: row passes run the last log R2 stages, column passes the
+    # first log R1
+    pb = polys * shard.nlimbs * (row_bflies(args.log_n) if "row" in dom
+                                 else (n // 2) * (args.log_n // 2))
+    fwd = "fwd" in dom
+    out["roofline_alu"] = roofline_alu(dom, pb if fwd else 0, 0 if fwd else pb, kavg[dom])
+    out["limiter"] = "valu" if out["roofline_alu"]["frac"] > out["roofline"]["frac"] else "hbm"
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_ntt(ctx.moduli, args.log_n, args.cpu_seconds)
