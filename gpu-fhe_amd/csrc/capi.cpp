@@ -29,9 +29,17 @@ int check_window(const fhe_ctx* c, uint32_t limb0, uint32_t nlimbs, uint32_t lim
 
 }  // namespace
 
-// Internal workspace (grows on demand; allocation makes this path non-capturable).
-int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws) {
+// Internal workspace (grows on demand).  Refused while `s` is capturing a graph: growing it would
+// free memory a captured graph still points at, and a graph sharing it with eager calls on other
+// streams would race them, so captured calls must bring their own workspace.
+int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws, hipStream_t s) {
   if (*ws) return kOk;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  FHE_HIP_CHECK(hipStreamIsCapturing(s, &st));
+  if (st != hipStreamCaptureStatusNone) {
+    set_error("workspace == NULL while the stream is capturing a graph: pass a workspace");
+    return kInvalid;
+  }
   auto* c = const_cast<fhe_ctx*>(cc);
   if (c->workspace_bytes < bytes) {
     if (c->workspace) FHE_HIP_CHECK(hipFree(c->workspace));
@@ -112,7 +120,7 @@ int fhe_ctx_reserve(fhe_ctx* c, size_t bytes) {
     return kInvalid;
   }
   void* ws = nullptr;
-  return ensure_ws(c, bytes, &ws);
+  return ensure_ws(c, bytes, &ws, nullptr);
 }
 
 static int vec_ctx(int op, const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint64_t* b,
@@ -153,19 +161,24 @@ int fhe_vec_op_mod(int op, uint64_t* out, const uint64_t* a, const uint64_t* b, 
     return kInvalid;
   }
   const uint64_t nm = mod_stride ? (rows - 1) * mod_stride + 1 : 1;
-  std::vector<ModParams> mp(nm);
-  for (uint64_t i = 0; i < nm; ++i) {
+  for (uint64_t i = 0; i < nm; ++i)
     if (mods[i] < 2) {
       set_error("fhe_vec_op_mod: modulus must be >= 2");
       return kInvalid;
     }
-    mp[i] = make_mod_params(mods[i]);
-  }
   FHE_HIP_CHECK(hipSetDevice(device));
+  if (nm <= (uint64_t)kArgMods) {  // the common case: moduli by value, nothing allocated or synced
+    ModArgs inl{};
+    for (uint64_t i = 0; i < nm; ++i) inl.m[i] = make_mod_params(mods[i]);
+    return launch_vec_mod(op, out, a, b, rows, cols, nullptr, inl, mod_stride, signed_in, hs(s));
+  }
+  std::vector<ModParams> mp(nm);
+  for (uint64_t i = 0; i < nm; ++i) mp[i] = make_mod_params(mods[i]);
   ModParams* d = nullptr;
   FHE_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d), nm * sizeof(ModParams), hs(s)));
   FHE_HIP_CHECK(hipMemcpyAsync(d, mp.data(), nm * sizeof(ModParams), hipMemcpyHostToDevice, hs(s)));
-  const int rc = launch_vec_mod(op, out, a, b, rows, cols, d, mod_stride, signed_in, hs(s));
+  const int rc = launch_vec_mod(op, out, a, b, rows, cols, d, ModArgs{}, mod_stride, signed_in,
+                                hs(s));
   FHE_HIP_CHECK(hipStreamSynchronize(hs(s)));  // mp must outlive the async copy
   FHE_HIP_CHECK(hipFreeAsync(d, hs(s)));
   return rc;
@@ -207,7 +220,7 @@ int fhe_hommult(const fhe_ctx* c, uint64_t* d, const uint64_t* a, const uint64_t
                 uint32_t batch, uint32_t limb0, uint32_t nlimbs, void* ws, fhe_stream_t s) {
   int rc = check_window(c, limb0, nlimbs, c ? c->L : 0, "fhe_hommult");
   if (rc) return rc;
-  if ((rc = ensure_ws(c, hommult_workspace_bytes(c, batch, nlimbs), &ws))) return rc;
+  if ((rc = ensure_ws(c, hommult_workspace_bytes(c, batch, nlimbs), &ws, hs(s)))) return rc;
   return launch_hommult(c, d, a, b, batch, limb0, nlimbs, ws, hs(s));
 }
 
@@ -230,7 +243,7 @@ int fhe_keyswitch_shard(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const ui
                         fhe_stream_t s) {
   int rc = check_window(c, limb0, nlimbs, c ? c->L : 0, "fhe_keyswitch_shard");
   if (rc) return rc;
-  if ((rc = ensure_ws(c, keyswitch_workspace_bytes(c, nlimbs, batch), &ws))) return rc;
+  if ((rc = ensure_ws(c, keyswitch_workspace_bytes(c, nlimbs, batch), &ws, hs(s)))) return rc;
   return launch_keyswitch_shard(c, ks0, ks1, c_all, d2_own, evk_b, evk_a, limb0, nlimbs, batch,
                                 ws, hs(s));
 }
@@ -241,7 +254,7 @@ int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t
   int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_keyswitch");
   if (rc) return rc;
   const size_t bytes = keyswitch_workspace_bytes(c, c->L, batch);
-  if ((rc = ensure_ws(c, bytes, &ws))) return rc;
+  if ((rc = ensure_ws(c, bytes, &ws, hs(s)))) return rc;
   // c_all = INTT(d2) lives at the tail of the workspace (out of place: no copy of d2)
   const size_t call = (size_t)batch * c->L * c->n * sizeof(uint64_t);
   uint64_t* c_all = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + bytes - call);
@@ -258,7 +271,7 @@ int fhe_rescale(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t po
                 uint32_t nlimbs, int ntt_form, void* ws, fhe_stream_t s) {
   int rc = check_window(c, 0, nlimbs, c ? c->L : 0, "fhe_rescale");
   if (rc) return rc;
-  if (ntt_form && (rc = ensure_ws(c, rescale_workspace_bytes(c, polys, nlimbs), &ws))) return rc;
+  if (ntt_form && (rc = ensure_ws(c, rescale_workspace_bytes(c, polys, nlimbs), &ws, hs(s)))) return rc;
   return launch_rescale(c, out, in, polys, nlimbs, ntt_form != 0, ws, hs(s));
 }
 
@@ -289,7 +302,7 @@ int fhe_rotate(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t gal
     set_error("fhe_rotate: out must not alias in");
     return kInvalid;
   }
-  if ((rc = ensure_ws(c, rotate_workspace_bytes(c, batch), &ws))) return rc;
+  if ((rc = ensure_ws(c, rotate_workspace_bytes(c, batch), &ws, hs(s)))) return rc;
   return launch_rotate(c, out, in, galois_elt, rot_b, rot_a, batch, ws, hs(s));
 }
 
@@ -302,7 +315,7 @@ int fhe_mul_relin(const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint
                   void* ws, fhe_stream_t s) {
   int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_mul_relin");
   if (rc) return rc;
-  if ((rc = ensure_ws(c, mul_relin_workspace_bytes(c, batch), &ws))) return rc;
+  if ((rc = ensure_ws(c, mul_relin_workspace_bytes(c, batch), &ws, hs(s)))) return rc;
   return launch_mul_relin(c, out, a, b, evk_b, evk_a, batch, rescale != 0, ws, hs(s));
 }
 

@@ -51,16 +51,20 @@ __device__ __forceinline__ u64 to_residue(u64 x, int signed_in, const ModParams&
   return reduce_u64(x, m);
 }
 
+// The generic kernel's moduli: up to kArgMods records travel in the kernel arguments (the
+// reference's scalar MOD or an (L, 1) column: no device allocation, no copy, no synchronisation,
+// so the call is graph-capturable); longer columns come from a device array.
 template <int OP>
 __global__ __launch_bounds__(kThreads) void k_vec_mod(u64* __restrict__ out,
                                                       const u64* __restrict__ a,
                                                       const u64* __restrict__ b, u64 rows,
                                                       u64 cols, const ModParams* __restrict__ mods,
-                                                      u64 mod_stride, int signed_in) {
+                                                      ModArgs inl, u64 mod_stride, int signed_in) {
   const u64 total = rows * cols;
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const ModParams m = mods[(i / cols) * mod_stride];
+    const u64 k = (i / cols) * mod_stride;
+    const ModParams m = mods ? mods[k] : inl.m[k];
     const u64 x = to_residue(a[i], signed_in, m), y = to_residue(b[i], signed_in, m);
     u64 r;
     if (OP == kAdd) r = x >= m.q - y ? x - (m.q - y) : x + y;
@@ -93,14 +97,15 @@ int launch_vec_ctx(const fhe_ctx* c, int op, u64* out, const u64* a, const u64* 
 }
 
 int launch_vec_mod(int op, u64* out, const u64* a, const u64* b, u64 rows, u64 cols,
-                   const ModParams* d_mods, u64 mod_stride, int signed_in, hipStream_t s) {
+                   const ModParams* d_mods, const ModArgs& inl, u64 mod_stride, int signed_in,
+                   hipStream_t s) {
   const u64 total = rows * cols;
   if (total == 0) return kOk;
   const u32 g = grid_for(total);
   switch (op) {
-    case kAdd: k_vec_mod<kAdd><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, mod_stride, signed_in); break;
-    case kSub: k_vec_mod<kSub><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, mod_stride, signed_in); break;
-    case kMul: k_vec_mod<kMul><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, mod_stride, signed_in); break;
+    case kAdd: k_vec_mod<kAdd><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, inl, mod_stride, signed_in); break;
+    case kSub: k_vec_mod<kSub><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, inl, mod_stride, signed_in); break;
+    case kMul: k_vec_mod<kMul><<<g, kThreads, 0, s>>>(out, a, b, rows, cols, d_mods, inl, mod_stride, signed_in); break;
     default: set_error("bad vec op"); return kInvalid;
   }
   FHE_HIP_CHECK(hipGetLastError());

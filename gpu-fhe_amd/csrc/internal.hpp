@@ -67,6 +67,10 @@ struct fhe_ctx {
 
   void* workspace = nullptr;
   size_t workspace_bytes = 0;
+  // fhe_baseconv's conversion tables per source range (s0, S): device [S] inv + [S][L + K] hat,
+  // built on first use (rns.hip launch_baseconv) and freed with the context
+  std::mutex bc_mutex;
+  std::vector<std::pair<uint64_t, ulonglong2*>> bc_tables;
   // helper stream for split-batch HomMult (created on first use; fork/join by events)
   hipStream_t aux_stream = nullptr;
   hipEvent_t aux_fork = nullptr, aux_join = nullptr;
@@ -135,8 +139,15 @@ size_t hommult_workspace_bytes(const fhe_ctx* c, u32 batch, u32 nlimbs);
 enum VecOp : int { kAdd = 0, kSub = 1, kMul = 2 };
 int launch_vec_ctx(const fhe_ctx* c, int op, u64* out, const u64* a, const u64* b, u32 polys,
                    u32 limb0, u32 nlimbs, hipStream_t s);
+// moduli records inline in the kernel arguments (generic vec ops with few distinct moduli)
+constexpr int kArgMods = 32;
+struct ModArgs {
+  ModParams m[kArgMods];
+};
+// row r uses d_mods[r * mod_stride], or inl.m[r * mod_stride] when d_mods is null
 int launch_vec_mod(int op, u64* out, const u64* a, const u64* b, u64 rows, u64 cols,
-                   const ModParams* d_mods, u64 mod_stride, int signed_in, hipStream_t s);
+                   const ModParams* d_mods, const ModArgs& inl, u64 mod_stride, int signed_in,
+                   hipStream_t s);
 
 // ---- launchers (rns.hip) --------------------------------------------------------------
 // Per-rank body of the hybrid key-switch (SURVEY.md §8a', §8e) over `batch` ciphertexts sharing
@@ -171,8 +182,9 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
                      const u64* evk_a, u32 batch, bool rescale, void* ws, hipStream_t s);
 size_t mul_relin_workspace_bytes(const fhe_ctx* c, u32 batch);
 
-// caller workspace, else the context's internal one grown to `bytes` (capi.cpp)
-int ensure_ws(const fhe_ctx* c, size_t bytes, void** ws);
+// caller workspace, else the context's internal one grown to `bytes` (capi.cpp); an error while
+// `s` is capturing a graph
+int ensure_ws(const fhe_ctx* c, size_t bytes, void** ws, hipStream_t s);
 
 // ---- host (context.cpp) ----------------------------------------------------------------
 int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 K, u32 dnum,

@@ -198,7 +198,7 @@ int fhe_encrypt(const fhe_ctx* c, uint64_t* ct, const uint64_t* pt, const uint64
   const hipStream_t s = static_cast<hipStream_t>(st);
   const u32 L = c->L;
   const u64 ln = (u64)L * c->n;
-  int rc0 = ensure_ws(c, ln * sizeof(u64), &ws);
+  int rc0 = ensure_ws(c, ln * sizeof(u64), &ws, s);
   if (rc0) return rc0;
   u64* u = static_cast<u64*>(ws);  // [L][N]
   u64* c0 = ct;

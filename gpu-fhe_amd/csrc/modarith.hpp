@@ -181,6 +181,15 @@ __device__ __forceinline__ u64 mont_reduce_lazy(u64 tlo, u64 thi, u64 q, u64 qin
   return thi + mulhi64(m, q) + (tlo != 0 ? 1 : 0);
 }
 
+// Subtractive Montgomery reduction (R = 2^64) of t = (thi, tlo) < q 2^64 with qi = q^-1 mod 2^64:
+// m = tlo qi makes m q = t mod 2^64, so t - m q is an exact multiple of 2^64 (no carry term, unlike
+// mont_reduce_lazy's t + m q) and (t - m q) / 2^64 = thi - hi64(m q) lies in (-q, q): returns
+// thi + q - hi64(m q) in (0, 2q), congruent to t R^-1.
+__device__ __forceinline__ u64 mont_redc(u64 tlo, u64 thi, u64 q, u64 qi) {
+  const u64 m = tlo * qi;
+  return (thi + q) - mulhi64(m, q);
+}
+
 // Sum of up to four products y_k h_k with y_k, h_k < 2^61, from 30-bit pieces (lo = v & (2^30 - 1),
 // hi = v >> 30 < 2^31): the partial products of each weight 1, 2^30, 2^60 sum in one 64-bit word
 // (4 < 2^62, 8 < 2^64, 4 < 2^64) with no carries, so a term costs four v_mad_u64_u32 instead of a

@@ -1041,20 +1041,23 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   if constexpr (H::POLY_MAJOR) grp = __builtin_amdgcn_readfirstlane(grp);
   const bool active = grp < 3;
   const u32 aoff = grp == 2 ? G::RS : 0, boff = grp == 2 ? 3 * G::RS : 2 * G::RS;
+  // subtractive REDC (mont_redc): no carry-in term, 3 VALU fewer per element than the additive one
+  u64 qi = 0 - m.qinv;  // q^-1 mod 2^64
+  asm("" : "+s"(qi));
   if (grp == 1) {
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
       const u32 idx = own.idx(tpT | LayT::jpos(j));
       const u128 t = (u128)rowlds[idx] * rowlds[3 * G::RS + idx] +
                      (u128)rowlds[G::RS + idx] * rowlds[2 * G::RS + idx];
-      v[j] = mont_reduce_lazy((u64)t, (u64)(t >> 64), q, m.qinv);
+      v[j] = mont_redc((u64)t, (u64)(t >> 64), q, qi);
     }
   } else if (active) {
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
       const u32 idx = own.idx(tpT | LayT::jpos(j));
       const u128 t = (u128)rowlds[aoff + idx] * rowlds[boff + idx];
-      v[j] = mont_reduce_lazy((u64)t, (u64)(t >> 64), q, m.qinv);
+      v[j] = mont_redc((u64)t, (u64)(t >> 64), q, qi);
     }
   }
   if constexpr (HR == 2) {  // the wide inverse takes canonical inputs

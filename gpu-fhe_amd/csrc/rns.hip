@@ -501,19 +501,27 @@ int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u3
     set_error("baseconv: limb ranges out of bounds or overlapping");
     return kInvalid;
   }
-  std::vector<ulonglong2> inv, hat;
-  conv_tables(c->moduli, s0, S, inv, hat);
+  // the (s0, S) tables, cached on the context: built, uploaded and synchronised once
   ulonglong2* d_tab = nullptr;
-  FHE_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d_tab), (inv.size() + hat.size()) * 16, s));
-  FHE_HIP_CHECK(hipMemcpyAsync(d_tab, inv.data(), inv.size() * 16, hipMemcpyHostToDevice, s));
-  FHE_HIP_CHECK(hipMemcpyAsync(d_tab + inv.size(), hat.data(), hat.size() * 16,
-                               hipMemcpyHostToDevice, s));
+  {
+    auto* cc = const_cast<fhe_ctx*>(c);
+    std::lock_guard<std::mutex> lock(cc->bc_mutex);
+    const uint64_t key = ((uint64_t)s0 << 32) | S;
+    for (auto& t : cc->bc_tables)
+      if (t.first == key) d_tab = t.second;
+    if (!d_tab) {
+      std::vector<ulonglong2> inv, hat;
+      conv_tables(c->moduli, s0, S, inv, hat);
+      FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_tab), (inv.size() + hat.size()) * 16));
+      cc->bc_tables.emplace_back(key, d_tab);
+      FHE_HIP_CHECK(hipMemcpyAsync(d_tab, inv.data(), inv.size() * 16, hipMemcpyHostToDevice, s));
+      FHE_HIP_CHECK(hipMemcpyAsync(d_tab + S, hat.data(), hat.size() * 16, hipMemcpyHostToDevice,
+                                   s));
+      FHE_HIP_CHECK(hipStreamSynchronize(s));  // the host vectors must outlive the copies
+    }
+  }
   const BcArgs a{in, 0, s0, out, 0, T, RowMap{T, t0, 0}, 0, 0, 1};
-  const int rc = baseconv_any(S, a, c->n, d_tab, d_tab + inv.size(), M, c->d_mods, c->wide, s);
-  // the host vectors must outlive the async copies
-  FHE_HIP_CHECK(hipStreamSynchronize(s));
-  FHE_HIP_CHECK(hipFreeAsync(d_tab, s));
-  return rc;
+  return baseconv_any(S, a, c->n, d_tab, d_tab + S, M, c->d_mods, c->wide, s);
 }
 
 }  // namespace fhe

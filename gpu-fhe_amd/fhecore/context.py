@@ -9,6 +9,7 @@ residues, layout [..., limb, N], on a HIP device.
 from __future__ import annotations
 
 import ctypes
+import threading
 from functools import lru_cache
 
 import numpy as np
@@ -87,6 +88,27 @@ def _check_tensor(t, what, shape_tail=None):
 
 # ----------------------------------------------------------------------------- context
 
+# Tensors allocated by this module while a Graph is capturing: the captured kernels keep their
+# addresses, so the Graph holds a reference to each (else the caching allocator would hand their
+# memory to other tensors while replays still write it).
+_CAPTURE = threading.local()
+
+
+def _keep(t):
+    keep = getattr(_CAPTURE, "keep", None)
+    if keep is not None:
+        keep.append(t)
+    return t
+
+
+def _empty(*args, **kw):
+    return _keep(torch.empty(*args, **kw))
+
+
+def _empty_like(*args, **kw):
+    return _keep(torch.empty_like(*args, **kw))
+
+
 class Context:
     """RNS-CKKS-style parameter context on one HIP device (wraps ``fhe_ctx``).
 
@@ -148,10 +170,10 @@ class Context:
         return torch.device("cuda", self.device)
 
     def empty(self, *shape):
-        return torch.empty(shape, dtype=torch.int64, device=self._dev())
+        return _empty(shape, dtype=torch.int64, device=self._dev())
 
     def workspace(self, nbytes: int):
-        return torch.empty((max(int(nbytes), 8) + 7) // 8, dtype=torch.int64, device=self._dev())
+        return _empty((max(int(nbytes), 8) + 7) // 8, dtype=torch.int64, device=self._dev())
 
     # -- NTT (replaces NTT / iNTT, arithmetic.py:15-19)
     def ntt_(self, t, limb0: int = 0):
@@ -172,7 +194,7 @@ class Context:
     def _ntt_to(self, t, out, limb0, fwd):
         _check_tensor(t, "ntt", (self.n,))
         if out is None:
-            out = torch.empty_like(t)
+            out = _empty_like(t)
         elif out.shape != t.shape or out.dtype != t.dtype or not out.is_contiguous():
             raise _capi.FheError("ntt: out must be a contiguous tensor shaped like the input")
         nl = t.shape[-2] if t.dim() >= 2 else 1
@@ -197,7 +219,7 @@ class Context:
         _check_tensor(b, op, (self.n,))
         if a.shape != b.shape:
             raise AssertionError("a.shape != b.shape")  # the reference asserts (arithmetic.py:4)
-        out = torch.empty_like(a) if out is None else out
+        out = _empty_like(a) if out is None else out
         nl = a.shape[-2] if a.dim() >= 2 else 1
         polys = a.numel() // (nl * self.n)
         fn = {"add": load().fhe_vec_add, "sub": load().fhe_vec_sub, "mul": load().fhe_vec_mul}[op]
@@ -247,7 +269,7 @@ class Context:
         if d2.shape[-2] != self.L:
             raise ValueError("keyswitch: d2 must be [..., L, N]")
         batch = d2.numel() // (self.L * self.n)
-        ks0, ks1 = torch.empty_like(d2), torch.empty_like(d2)
+        ks0, ks1 = _empty_like(d2), _empty_like(d2)
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
             lib.fhe_keyswitch_workspace(self._ptr, self.L, batch))
@@ -268,7 +290,7 @@ class Context:
         _check_tensor(x, "x", (self.n,))
         nl = x.shape[-2]
         polys = x.numel() // (nl * self.n)
-        out = torch.empty(*x.shape[:-2], nl - 1, self.n, dtype=x.dtype, device=x.device)
+        out = _empty(*x.shape[:-2], nl - 1, self.n, dtype=x.dtype, device=x.device)
         lib = load()
         ws = None
         if ntt_form:
@@ -284,7 +306,7 @@ class Context:
         _check_tensor(x, "x", (self.n,))
         nl = x.shape[-2]
         polys = x.numel() // (nl * self.n)
-        out = torch.empty_like(x)
+        out = _empty_like(x)
         with torch.cuda.device(self.device):
             check(load().fhe_automorphism(self._ptr, _ptr(out), _ptr(x), polys, limb0, nl,
                                           galois_elt, int(ntt_form), _stream(x)), "fhe_automorphism")
@@ -297,7 +319,7 @@ class Context:
         if tuple(rot_b.shape) != (self.dnum, self.L + self.K, self.n) or rot_a.shape != rot_b.shape:
             raise ValueError("rotate: key must be [dnum, L + K, N]")
         batch = ct.numel() // (2 * self.L * self.n)
-        out = torch.empty_like(ct)
+        out = _empty_like(ct)
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
             lib.fhe_rotate_workspace(self._ptr, batch))
@@ -312,7 +334,7 @@ class Context:
     def sample(self, kind: str, polys: int, seed: int, tag: int, limb0: int = 0, nlimbs=None):
         """[polys, nlimbs, N] residues of a Philox4x32-10 draw (oracle: pyoracle.sample)."""
         nl = (self.L + self.K - limb0) if nlimbs is None else nlimbs
-        out = torch.empty(polys, nl, self.n, dtype=torch.int64, device=self._dev())
+        out = _empty(polys, nl, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_sample(self._ptr, _ptr(out), polys, limb0, nl, self.KIND[kind],
                                     seed, tag, _stream(out)), "fhe_sample")
@@ -320,13 +342,13 @@ class Context:
 
     def keygen_secret(self, seed: int):
         """Ternary secret, NTT form over all L + K limbs: [L + K, N]."""
-        sk = torch.empty(self.L + self.K, self.n, dtype=torch.int64, device=self._dev())
+        sk = _empty(self.L + self.K, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_keygen_secret(self._ptr, _ptr(sk), seed, _stream(sk)), "fhe_keygen_secret")
         return sk
 
     def keygen_public(self, sk, seed: int):
-        pk = torch.empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
+        pk = _empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_keygen_public(self._ptr, _ptr(pk), _ptr(sk), seed, _stream(pk)),
                   "fhe_keygen_public")
@@ -335,7 +357,7 @@ class Context:
     def keygen_switch(self, sk, s_from, seed: int):
         """Key-switch key from s_from ([L + K, N] NTT form) to sk: (evk_b, evk_a), each
         [dnum, L + K, N] -- the operands of keyswitch / rotate / mul_relin."""
-        key = torch.empty(2, self.dnum, self.L + self.K, self.n, dtype=torch.int64, device=self._dev())
+        key = _empty(2, self.dnum, self.L + self.K, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_keygen_switch(self._ptr, _ptr(key), _ptr(sk), _ptr(s_from), seed,
                                            _stream(key)), "fhe_keygen_switch")
@@ -343,7 +365,7 @@ class Context:
 
     def keygen_relin(self, sk, seed: int):
         """Relinearisation key: switches s^2 to s."""
-        s2 = torch.empty_like(sk)
+        s2 = _empty_like(sk)
         lib = load()
         with torch.cuda.device(self.device):
             check(lib.fhe_vec_mul(self._ptr, _ptr(s2), _ptr(sk), _ptr(sk), 1, 0, self.L + self.K,
@@ -356,14 +378,15 @@ class Context:
 
     def encrypt(self, pt, pk, seed: int):
         """Public-key encryption of an NTT-form plaintext [L, N] -> ciphertext [2, L, N]."""
-        ct = torch.empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
+        ct = _empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
-            check(load().fhe_encrypt(self._ptr, _ptr(ct), _ptr(pt), _ptr(pk), seed, None,
+            ws = self.workspace(self.L * self.n * 8)  # a Graph keeps it (no internal workspace)
+            check(load().fhe_encrypt(self._ptr, _ptr(ct), _ptr(pt), _ptr(pk), seed, _ptr(ws),
                                      _stream(ct)), "fhe_encrypt")
         return ct
 
     def encrypt_sk(self, pt, sk, seed: int):
-        ct = torch.empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
+        ct = _empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_encrypt_sk(self._ptr, _ptr(ct), _ptr(pt), _ptr(sk), seed, _stream(ct)),
                   "fhe_encrypt_sk")
@@ -374,7 +397,7 @@ class Context:
         _check_tensor(ct, "ct", (self.n,))
         nl = ct.shape[-2]
         batch = ct.numel() // (2 * nl * self.n)
-        pt = torch.empty(*ct.shape[:-3], nl, self.n, dtype=ct.dtype, device=ct.device)
+        pt = _empty(*ct.shape[:-3], nl, self.n, dtype=ct.dtype, device=ct.device)
         with torch.cuda.device(self.device):
             check(load().fhe_decrypt(self._ptr, _ptr(pt), _ptr(ct), _ptr(sk), batch, nl, _stream(ct)),
                   "fhe_decrypt")
@@ -393,7 +416,7 @@ class Context:
         batch = a.numel() // (2 * self.L * self.n)
         shape = (*a.shape[:-2], self.L - (1 if rescale else 0), self.n)
         if out is None:
-            out = torch.empty(shape, dtype=a.dtype, device=a.device)
+            out = _empty(shape, dtype=a.dtype, device=a.device)
         elif tuple(out.shape) != shape:
             raise ValueError(f"mul_relin: out must be {shape}")
         lib = load()
@@ -427,7 +450,7 @@ class Context:
         check(lib.fhe_deserialize(self._ptr, blob, len(blob), None, 0, ctypes.byref(polys),
                                   ctypes.byref(limb0), ctypes.byref(nl), ctypes.byref(ntt), None),
               "fhe_deserialize")
-        out = torch.empty(polys.value, nl.value, self.n, dtype=torch.int64, device=self._dev())
+        out = _empty(polys.value, nl.value, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(lib.fhe_deserialize(self._ptr, blob, len(blob), _ptr(out), out.numel(), None, None,
                                       None, None, _stream(out)), "fhe_deserialize")
@@ -444,7 +467,7 @@ class Context:
             raise ValueError("keyswitch_shard: c_all must be [batch, L, N]")
         if tuple(evk_b.shape) != (self.dnum, nl + self.K, self.n) or evk_a.shape != evk_b.shape:
             raise ValueError("keyswitch_shard: evk slices must be [dnum, nlimbs + K, N]")
-        ks0, ks1 = torch.empty_like(d2_own), torch.empty_like(d2_own)
+        ks0, ks1 = _empty_like(d2_own), _empty_like(d2_own)
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
             lib.fhe_keyswitch_workspace(self._ptr, nl, batch))
@@ -457,8 +480,12 @@ class Context:
 
 class Graph:
     """Capture libfhecore calls issued on the current stream into a HIP graph and replay them
-    (fhe_graph_*).  Every call inside the block needs an explicit (preallocated) workspace or one
-    eager run beforehand; the tensors used are baked into the graph::
+    (fhe_graph_*).  The tensors a captured call reads and writes are baked into the graph:
+    outputs and workspaces that the Context methods allocate inside the block are kept alive by
+    the Graph (``Graph.tensors``; read results from there or pass ``out=``), and caller-owned
+    tensors must outlive it.  Every call is given a workspace -- the one passed in, or one this
+    module allocates and the Graph keeps -- since the context's internal one is refused while
+    capturing (include/fhecore.h)::
 
         with fhecore.Graph() as g:
             ctx.mul_relin(a, b, kb, ka, workspace=ws, out=out)
@@ -467,13 +494,16 @@ class Graph:
 
     def __init__(self):
         self._g = None
+        self.tensors = []
 
     def __enter__(self):
         self._stream = torch.cuda.current_stream()
         check(load().fhe_graph_begin(ctypes.c_void_p(self._stream.cuda_stream)), "fhe_graph_begin")
+        _CAPTURE.keep = self.tensors
         return self
 
     def __exit__(self, exc_type, exc, tb):
+        _CAPTURE.keep = None
         g = ctypes.c_void_p()
         rc = load().fhe_graph_end(ctypes.c_void_p(self._stream.cuda_stream), ctypes.byref(g))
         if exc_type is None:

@@ -86,7 +86,9 @@ int fhe_vec_mul(const fhe_ctx* ctx, uint64_t* out, const uint64_t* a, const uint
  * row r uses modulus mods[r * mod_stride] (mod_stride 0 = one scalar MOD).  `mods` is a HOST
  * array; inputs may be any uint64 (signed_in = 1: any int64), moduli any value in [2, 2^64).
  * Result = Python's exact (a op b) % MOD.  op: 0 add, 1 sub, 2 mul.
- * Allocates a small stream-ordered table (not capture-safe). */
+ * Up to 32 distinct modulus records (a scalar MOD, or a column of <= 32 rows) travel in the
+ * kernel arguments: no allocation or synchronisation, capture-safe.  Longer modulus columns
+ * allocate a stream-ordered table and synchronise `stream`. */
 int fhe_vec_op_mod(int op, uint64_t* out, const uint64_t* a, const uint64_t* b, uint64_t rows,
                    uint64_t cols, const uint64_t* mods, uint64_t mod_stride, int signed_in,
                    int device, fhe_stream_t stream);
@@ -120,7 +122,9 @@ int fhe_hommult(const fhe_ctx* ctx, uint64_t* d, const uint64_t* a, const uint64
 
 /* ---- RNS base conversion ---------------------------------------------------------------
  * Fast basis extension (no correction) from ctx limbs [s0, s0+S) to [t0, t0+T) (disjoint),
- * coefficient domain: in [S][N] -> out [T][N].  S <= 16.  Synchronises `stream`. */
+ * coefficient domain: in [S][N] -> out [T][N].  S <= 16.  The conversion tables of a
+ * (s0, S) source range are built and uploaded on its first use and cached on the context (that
+ * first call synchronises `stream`); later calls neither allocate nor synchronise. */
 int fhe_baseconv(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t s0, uint32_t S,
                  uint32_t t0, uint32_t T, fhe_stream_t stream);
 
@@ -216,9 +220,11 @@ int fhe_mul_relin(const fhe_ctx* ctx, uint64_t* out, const uint64_t* a, const ui
                   void* workspace, fhe_stream_t stream);
 
 /* ---- HIP graphs: capture a sequence of libfhecore calls on `stream` and replay it -----------
- * Between fhe_graph_begin and fhe_graph_end every call must be given an explicit workspace (or
- * have run once eagerly so the internal one is large enough): nothing may allocate or
- * synchronise while the stream is capturing.  Replays reuse the captured pointers. */
+ * Between fhe_graph_begin and fhe_graph_end every call that takes a workspace must be given an
+ * explicit one: with workspace == NULL a call returns FHE_EINVAL while the stream is capturing
+ * (the context's internal workspace may be reallocated later, which would leave the graph
+ * pointing at freed memory).  Replays reuse the captured pointers, so every buffer a captured
+ * call touches must outlive the graph. */
 typedef struct fhe_graph_s* fhe_graph_t;
 int fhe_graph_begin(fhe_stream_t stream);
 int fhe_graph_end(fhe_stream_t stream, fhe_graph_t* graph);

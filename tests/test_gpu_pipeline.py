@@ -112,3 +112,44 @@ def test_graph_replay_matches_eager(fc):
         g.launch()
     stream.synchronize()
     assert (fc.to_host(out) == eager).all()
+
+
+def test_graph_keeps_its_allocations_and_refuses_internal_workspace(fc):
+    """a graph captured without workspace=/out= must not reference memory that is
+    freed and reused after capture.  The Context's own allocations inside the block are kept by
+    the Graph; replays after heavy allocation churn still reproduce the eager result.  At the C
+    ABI a NULL workspace is refused while capturing (the internal workspace could be regrown)."""
+    import ctypes
+
+    import torch
+    from fhecore.context import _ptr
+
+    log_n, L = 12, 3
+    ctx = fc.Context(log_n, L=L)
+    d = fc.to_device
+    a, b = d(rand(ctx.moduli, log_n, (2, 2), seed=15)), d(rand(ctx.moduli, log_n, (2, 2), seed=16))
+    eager = fc.to_host(ctx.hommult(a, b))
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        with fc.Graph() as g:
+            out = ctx.hommult(a, b)  # output and workspace allocated inside the capture
+        assert any(t.data_ptr() == out.data_ptr() for t in g.tensors) and len(g.tensors) >= 2
+        del out
+        junk = [torch.full((1 << 20,), -1, dtype=torch.int64, device=a.device) for _ in range(8)]
+        g.launch()
+        g.launch()
+    stream.synchronize()
+    assert all((j == -1).all() for j in junk)  # replays wrote only the graph's own buffers
+    assert (fc.to_host(g.tensors[0]) == eager).all()
+    # the C ABI: workspace == NULL during capture -> FHE_EINVAL, and the capture still ends cleanly
+    lib = fc.load()
+    dst = ctx.empty(2, 3, L, 1 << log_n)
+    with torch.cuda.stream(stream):
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        assert lib.fhe_graph_begin(sp) == 0
+        rc = lib.fhe_hommult(ctx.handle, _ptr(dst), _ptr(a), _ptr(b), 2, 0, L, None, sp)
+        gr = ctypes.c_void_p()
+        lib.fhe_graph_end(sp, ctypes.byref(gr))
+        if gr.value:
+            lib.fhe_graph_destroy(gr)
+    assert rc != 0 and "capturing" in lib.fhe_last_error().decode()
