@@ -7,6 +7,7 @@
 #include <mutex>
 #include <vector>
 
+#include "host_tables.hpp"
 #include "modarith.hpp"
 
 namespace fhe {
@@ -192,11 +193,6 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
 int ctx_destroy(fhe_ctx* c);
 int gen_moduli(u32 log_n, u32 count, u32 bits, u32 skip, u64* out);
 int build_rns_tables(fhe_ctx* c);
-ModParams make_mod_params(u64 q);
-bool is_prime_u64(u64 n);
-u64 powmod_u64(u64 b, u64 e, u64 q);
-u64 mulmod_u64(u64 a, u64 b, u64 q);
-u64 find_psi(u64 q, u32 log_n);
 
 }  // namespace fhe
 

@@ -18,23 +18,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "modparams.hpp"
+
 namespace fhe {
-
-using u64 = uint64_t;
-using u32 = uint32_t;
-using u128 = unsigned __int128;
-
-// Per-modulus constants, one record per RNS limb (device and host share the layout).
-struct ModParams {
-  u64 q;
-  u64 mu;    // Barrett: floor(2^(2 bitlen + 2) / q)
-  u32 sh_a;  // bitlen - 1
-  u32 sh_b;  // bitlen + 3  (= b - a)
-  u64 qinv;  // Montgomery (R = 2^64): -q^-1 mod 2^64 for odd q, else 0
-  u64 r64;   // 2^64 mod q, and its Shoup companion floor(r64 2^64 / q)
-  u64 r64s;
-  u64 ones;  // floor(2^64 / q): the Shoup companion of 1 (a 64-bit word mod q)
-};
 
 __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return (u64)(((u128)a * b) >> 64); }
 

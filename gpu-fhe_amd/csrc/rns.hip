@@ -35,13 +35,6 @@ struct RowMap {
   __host__ __device__ u32 limb(u32 r) const { return r < n0 ? base0 + r : base1 + (r - n0); }
 };
 
-inline ulonglong2 shoup_pair(u64 w, u64 q) {
-  ulonglong2 p;
-  p.x = w;
-  p.y = (u64)(((u128)w << 64) / q);
-  return p;
-}
-
 // in: S rows (stride N) over ctx limbs src0..src0+S-1; out: T rows (stride N), row r over
 // ctx limb map.limb(r); rows whose limb lies in [skip_lo, skip_hi) are left untouched.
 // inv[k] = (S^_k)^-1 mod s_k; hat[k * hs + limb] = S^_k mod limb.  Batch b = blockIdx.y reads
@@ -221,36 +214,13 @@ __global__ __launch_bounds__(kThreads) void k_modup_scale(const u64* __restrict_
       csub(shoup_lazy(in[(u64)b * in_bs + (u64)k * n + i], w.x, w.y, q), q);
 }
 
-template <class T>
-int upload(T** dptr, const std::vector<T>& v) {
+// host Shoup-pair table -> device ulonglong2 array (same 16-byte layout)
+int upload(ulonglong2** dptr, const std::vector<Pair64>& v) {
+  static_assert(sizeof(Pair64) == sizeof(ulonglong2), "table entry layout");
   if (v.empty()) return kOk;
-  FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(dptr), v.size() * sizeof(T)));
-  FHE_HIP_CHECK(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(dptr), v.size() * sizeof(Pair64)));
+  FHE_HIP_CHECK(hipMemcpy(*dptr, v.data(), v.size() * sizeof(Pair64), hipMemcpyHostToDevice));
   return kOk;
-}
-
-// (S^_k)^-1 mod s_k and S^_k mod t for a source set and every ctx limb t.
-void conv_tables(const std::vector<u64>& mods, u32 s0, u32 S, std::vector<ulonglong2>& inv,
-                 std::vector<ulonglong2>& hat) {
-  const u32 M = (u32)mods.size();
-  inv.resize(S);
-  hat.resize((size_t)S * M);
-  for (u32 k = 0; k < S; ++k) {
-    const u64 sk = mods[s0 + k];
-    u64 h = 1;
-    for (u32 i = 0; i < S; ++i)
-      if (i != k) h = mulmod_u64(h, mods[s0 + i] % sk, sk);
-    inv[k] = shoup_pair(powmod_u64(h, sk - 2, sk), sk);
-    for (u32 t = 0; t < M; ++t) {
-      const u64 tm = mods[t];
-      u64 hm = 1;
-      for (u32 i = 0; i < S; ++i)
-        if (i != k) hm = mulmod_u64(hm, mods[s0 + i] % tm, tm);
-      // {S^_k mod t, S^_k 2^64 mod t}: the plain word for the 128-bit sums of k_baseconv (S >= 8),
-      // the Montgomery form for its Montgomery-reduced sums (S < 8)
-      hat[(size_t)k * M + t] = ulonglong2{hm, (u64)(((u128)hm << 64) % tm)};
-    }
-  }
 }
 
 // One base conversion launch over `batch` independent inputs (strides in_bs / out_bs words).
@@ -320,16 +290,16 @@ int build_rns_tables(fhe_ctx* c) {
     set_error("ctx_create: key-switch needs alpha <= 16 and K <= 16");
     return kUnsupported;
   }
-  std::vector<ulonglong2> up_inv((size_t)c->dnum * alpha), up_hat((size_t)c->dnum * alpha * M);
+  std::vector<Pair64> up_inv((size_t)c->dnum * alpha), up_hat((size_t)c->dnum * alpha * M);
   for (u32 j = 0; j < c->dnum; ++j) {
     const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
     if (lo >= L) break;
-    std::vector<ulonglong2> inv, hat;
+    std::vector<Pair64> inv, hat;
     conv_tables(c->moduli, lo, hi - lo, inv, hat);
     std::copy(inv.begin(), inv.end(), up_inv.begin() + (size_t)j * alpha);
     std::copy(hat.begin(), hat.end(), up_hat.begin() + (size_t)j * alpha * M);
   }
-  std::vector<ulonglong2> dn_inv, dn_hat, pinv(L);
+  std::vector<Pair64> dn_inv, dn_hat, pinv(L);
   conv_tables(c->moduli, L, K, dn_inv, dn_hat);
   for (u32 i = 0; i < L; ++i) {
     const u64 q = c->moduli[i];
@@ -338,7 +308,7 @@ int build_rns_tables(fhe_ctx* c) {
     pinv[i] = shoup_pair(powmod_u64(pm, q - 2, q), q);
   }
   // ModDown's P-row INTT folds the conversion's (P^_k)^-1 into its last stage (N^-1 fold)
-  std::vector<ulonglong2> nf_down((size_t)4 * M, ulonglong2{0, 0});
+  std::vector<Pair64> nf_down((size_t)4 * M, Pair64{0, 0});
   for (u32 k = 0; k < K; ++k) {
     const u64 p = c->moduli[L + k];
     const u64 s = mulmod_u64(powmod_u64(c->n % p, p - 2, p), dn_inv[k].x, p);  // N^-1 (P^_k)^-1
@@ -510,7 +480,7 @@ int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u3
     for (auto& t : cc->bc_tables)
       if (t.first == key) d_tab = t.second;
     if (!d_tab) {
-      std::vector<ulonglong2> inv, hat;
+      std::vector<Pair64> inv, hat;
       conv_tables(c->moduli, s0, S, inv, hat);
       FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_tab), (inv.size() + hat.size()) * 16));
       cc->bc_tables.emplace_back(key, d_tab);
