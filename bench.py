@@ -120,27 +120,47 @@ def timed(fn, args, world, max_marks):
     return max_over_ranks(dt, world), {k: sum(v) / len(v) for k, v in per.items()}
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
 def cpu_baseline_hommult(moduli, log_n, budget_s):
-    """Exact C restatement (oracle/, test infrastructure) timed on this host: HomMult/s."""
+    """The tuned CPU port (oracle/fhe_cpu_port.c: lazy Harvey NTTs with Shoup twiddles,
+    Montgomery tensor, no 128-bit division, no per-limb allocation; OpenMP over (ciphertext,
+    limb)), bit-exact with the checker (tests/test_oracle.py), timed on this host: HomMult/s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle  # noqa: E402
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = cpu_threads()
     rng = np.random.default_rng(0)
-    n, L, B = 1 << log_n, len(moduli), 2
+    n, L, B = 1 << log_n, len(moduli), max(4, threads // 2)
     a = np.stack([np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in moduli])
                   for _ in range(2 * B)]).reshape(B, 2, L, n)
     b = a[::-1].copy()
-    coracle.hommult(a[:1], b[:1], moduli)  # build the twiddle tables outside the sample
+    d = np.empty((B, 3, L, n), dtype=np.uint64)
+    coracle.port_hommult_into(d[:1], a[:1], b[:1], moduli)  # twiddle tables outside the sample
     t0 = time.perf_counter()
     done = 0
     while time.perf_counter() - t0 < budget_s:
-        coracle.hommult(a, b, moduli)
+        coracle.port_hommult_into(d, a, b, moduli)
         done += B
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 2), "unit": "HomMult/s", "cores": threads, "kind": "port",
-            "sample": f"{done} HomMults (N=2^{log_n}, L={L}; exact C restatement "
-                      f"oracle/fhe_oracle.c, OpenMP {threads} threads) in {dt:.1f} s"}
+            "cpu_model": cpu_model(),
+            "sample": f"{done} HomMults (N=2^{log_n}, L={L}, batches of {B}) by the tuned C port "
+                      f"oracle/fhe_cpu_port.c (bit-exact with the checker), OpenMP {threads} "
+                      f"threads, in {dt:.1f} s"}
 
 
 def traffic_from_profile(kernel, shape):
@@ -320,26 +340,32 @@ def run_ntt(args, world, rank):
 
 
 def cpu_baseline_ntt(moduli, log_n, budget_s):
-    """Exact C restatement (oracle/, test infrastructure) timed on this host: forward NTT/s over
-    single-limb transforms (OpenMP across poly-limbs)."""
+    """The tuned CPU port (oracle/fhe_cpu_port.c) timed on this host: forward + inverse NTT/s over
+    single-limb transforms (OpenMP across poly-limbs), the GPU leg's unit of work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle  # noqa: E402
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = cpu_threads()
     rng = np.random.default_rng(0)
-    n, P = 1 << log_n, 4
+    n, P = 1 << log_n, max(4, threads // 2)
     mods = list(moduli)
     x = np.stack([np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in mods]) for _ in range(P)])
-    coracle.ntt_fwd(x[:1], mods)  # twiddle tables outside the sample
+    m = np.asarray(mods, dtype=np.uint64)
+    lib = coracle.lib()
+    p = coracle._p(x)
+    lib.port_ntt_fwd(coracle._p(x[:1].copy()), 1, log_n, coracle._p(m), len(mods))  # tables
     t0 = time.perf_counter()
     done = 0
     while time.perf_counter() - t0 < budget_s:
-        coracle.ntt_fwd(x, mods)
-        done += P * len(mods)
+        lib.port_ntt_fwd(p, P, log_n, coracle._p(m), len(mods))
+        lib.port_ntt_inv(p, P, log_n, coracle._p(m), len(mods))
+        done += 2 * P * len(mods)
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 1), "unit": "NTT/s", "cores": threads, "kind": "port",
-            "sample": f"{done} forward NTTs (N=2^{log_n}, {len(mods)} limbs x {P} polys per call; "
-                      f"exact C restatement oracle/fhe_oracle.c, OpenMP {threads} threads) in {dt:.1f} s"}
+            "cpu_model": cpu_model(),
+            "sample": f"{done} forward+inverse NTTs (N=2^{log_n}, {len(mods)} limbs x {P} polys per "
+                      f"call) by the tuned C port oracle/fhe_cpu_port.c, OpenMP {threads} threads, "
+                      f"in {dt:.1f} s"}
 
 
 def cpu_baseline_keyswitch(moduli, special, log_n, dnum, budget_s):
@@ -348,7 +374,7 @@ def cpu_baseline_keyswitch(moduli, special, log_n, dnum, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle  # noqa: E402
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = cpu_threads()
     rng = np.random.default_rng(2)
     n = 1 << log_n
     allm = list(moduli) + list(special)
@@ -362,8 +388,9 @@ def cpu_baseline_keyswitch(moduli, special, log_n, dnum, budget_s):
         done += 1
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 2), "unit": "keyswitch/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{done} key-switches (N=2^{log_n}, L={len(moduli)}, K={len(special)}, "
-                      f"dnum={dnum}; exact C restatement oracle/fhe_oracle.c, OpenMP {threads} "
+                      f"dnum={dnum}; the exact checker oracle/fhe_oracle.c -- no tuned key-switch port yet -- OpenMP {threads} "
                       f"threads) in {dt:.1f} s"}
 
 

@@ -47,6 +47,11 @@ def lib():
         L.oracle_keyswitch.argtypes = [_u64p, _u64p, _u64p, _u64p, _u64p, u32, _u64p, u32, _u64p,
                                        u32, u32]
         L.oracle_keyswitch.restype = None
+        for f in (L.port_ntt_fwd, L.port_ntt_inv):
+            f.argtypes = [_u64p, u64, u32, _u64p, u32]
+            f.restype = None
+        L.port_hommult.argtypes = [_u64p, _u64p, _u64p, u64, u32, _u64p, u32]
+        L.port_hommult.restype = None
         _lib = L
     return _lib
 
@@ -118,6 +123,37 @@ def hommult(a, b, moduli) -> np.ndarray:
     m = _u64(moduli)
     lib().oracle_hommult(_p(d), _p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(b)), B,
                          n.bit_length() - 1, _p(m), L)
+    return d[0] if squeeze else d
+
+
+# -- the tuned CPU port (oracle/fhe_cpu_port.c): bench.py's cpu_baseline, checked against the
+# exact functions above by tests/test_oracle.py
+
+def port_ntt(x, moduli, forward=True) -> np.ndarray:
+    """In-place style on a copy: the port's lazy Harvey NTT (forward) or GS inverse."""
+    x = _u64(x).copy()
+    m = _u64(moduli)
+    L, n = x.shape[-2], x.shape[-1]
+    assert m.size == L
+    fn = lib().port_ntt_fwd if forward else lib().port_ntt_inv
+    fn(_p(x), x.size // (L * n), n.bit_length() - 1, _p(m), L)
+    return x
+
+
+def port_hommult_into(d, a, b, moduli) -> None:
+    """d[B, 3, L, N] = HomMult(a, b) by the tuned port; no allocation (the timed call)."""
+    B, _, L, n = a.shape
+    lib().port_hommult(_p(d), _p(a), _p(b), B, n.bit_length() - 1, _p(_u64(moduli)), L)
+
+
+def port_hommult(a, b, moduli) -> np.ndarray:
+    a = _u64(a)
+    b = _u64(b)
+    squeeze = a.ndim == 3
+    if squeeze:
+        a, b = a[None], b[None]
+    d = np.empty((a.shape[0], 3) + a.shape[2:], dtype=np.uint64)
+    port_hommult_into(d, np.ascontiguousarray(a), np.ascontiguousarray(b), moduli)
     return d[0] if squeeze else d
 
 

@@ -253,3 +253,22 @@ def test_sampler_distributions():
     assert max(abs(v) for v in e) <= 21 and abs(np.mean(e)) < 0.2 and abs(np.var(e) - 10.5) < 1.0
     u = [int(v) for v in pyoracle.sample("uniform", 7, 2, 0, [(0, q)], n)[0]]
     assert all(0 <= v < q for v in u) and abs(np.mean(u) / q - 0.5) < 0.02
+
+
+# ---- the tuned CPU port (bench.py's cpu_baseline) is bit-exact with the checker ---------------
+
+@pytest.mark.parametrize("log_n,bits", [(10, 60), (12, 55), (13, 61), (11, 50)])
+def test_cpu_port_matches_oracle(log_n, bits):
+    import coracle
+
+    mods = coracle.gen_moduli(log_n, 3, bits=bits)
+    rng = np.random.default_rng(log_n + bits)
+    n = 1 << log_n
+    x = np.stack([rng.integers(0, q, (2, n), dtype=np.uint64) for q in mods], axis=1)
+    x[0, :, :8] = np.asarray(mods, dtype=np.uint64)[:, None] - 1
+    f = coracle.ntt_fwd(x, mods)
+    assert (coracle.port_ntt(x, mods, True) == f).all()
+    assert (coracle.port_ntt(f, mods, False) == x).all()
+    a = np.stack([rng.integers(0, q, (2, 2, n), dtype=np.uint64) for q in mods], axis=2)
+    b = np.stack([rng.integers(0, q, (2, 2, n), dtype=np.uint64) for q in mods], axis=2)
+    assert (coracle.port_hommult(a, b, mods) == coracle.hommult(a, b, mods)).all()
