@@ -158,6 +158,24 @@ int launch_vec_mod(int op, u64* out, const u64* a, const u64* b, u64 rows, u64 c
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_all,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
                            u32 nlimbs, u32 batch, void* ws, hipStream_t s);
+// Where a key-switch finds the coefficient-form d2 of every Q-limb: element (b, l, i) at
+// ptr + b bs + (l / lpr) rs + (l % lpr) N + i.  Contiguous [batch][L][N]: lpr = L, bs = L N.
+// The rank-major output of an all-gather over G ranks of c = ceil(L / G) limbs each,
+// [G][batch][c][N] (the last ranks' blocks padded): lpr = c, rs = batch c N, bs = c N.
+struct CAll {
+  const u64* ptr;
+  u32 lpr;
+  u64 rs, bs;
+  static CAll contiguous(const u64* p, u32 L, u64 n) { return CAll{p, L, 0, (u64)L * n}; }
+  static CAll ranked(const u64* p, u32 L, u32 ranks, u32 batch, u64 n) {
+    const u32 c = (L + ranks - 1) / ranks;
+    return CAll{p, c, (u64)batch * c * n, (u64)c * n};
+  }
+  u64 off(u32 l, u64 n) const { return (u64)(l / lpr) * rs + (u64)(l % lpr) * n; }
+};
+int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
+                           const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
+                           u32 nlimbs, u32 batch, void* ws, hipStream_t s);
 size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch);
 // Fast basis extension between contiguous ctx limb ranges: in [S][N] over limbs [s0, s0+S),
 // out [T][N] over limbs [t0, t0+T) (ranges disjoint).

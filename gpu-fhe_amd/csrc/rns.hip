@@ -19,6 +19,17 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxSrc = 16;
+// Word offsets of a conversion's S source rows within one ciphertext (kernel argument): rows need
+// not be contiguous -- the rank-major all-gather output of the sharded key-switch puts a digit's
+// limbs in different rank blocks (CAll).
+struct KOff {
+  u64 o[kMaxSrc];
+};
+inline KOff rows_contiguous(u32 S, u64 n) {
+  KOff k{};
+  for (u32 i = 0; i < S; ++i) k.o[i] = (u64)i * n;
+  return k;
+}
 #ifndef FHE_KS_FUSED
 #define FHE_KS_FUSED 1
 #endif
@@ -49,7 +60,8 @@ struct RowMap {
 constexpr int kMaxRows = 64;
 template <int S, bool WIDE>
 __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ in, u64 in_bs,
-                                                       u32 src0, u64* __restrict__ out, u64 out_bs,
+                                                       KOff koff, u32 src0, u64* __restrict__ out,
+                                                       u64 out_bs,
                                                        u32 T, RowMap map, u32 skip_lo, u32 skip_hi,
                                                        u64 n, const ulonglong2* __restrict__ inv,
                                                        const ulonglong2* __restrict__ hat, u32 hs,
@@ -77,7 +89,7 @@ __global__ __launch_bounds__(kThreads) void k_baseconv(const u64* __restrict__ i
   for (int k = 0; k < S; ++k) {
     const u64 qk = mods[src0 + k].q;
     const ulonglong2 w = inv[k];
-    y[k] = csub(shoup_lazy(in[(u64)k * n + i], w.x, w.y, qk), qk);
+    y[k] = csub(shoup_lazy(in[koff.o[k] + i], w.x, w.y, qk), qk);
     if constexpr (kSplit) y[k] = split30(y[k]);
   }
   for (u32 r = 0; r < T; ++r) {
@@ -198,10 +210,11 @@ __global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ o
 }
 
 // Prologue of the fused conversion column pass (ntt.hip k_modup_col), ModUp and ModDown:
-// y[b][k][i] = [x_k (D^_k)^-1]_{d_k} over S consecutive source rows in[b][k] (batch stride in_bs)
-// whose moduli are mods[mod0 + k].  Grid: x over coefficients, y = k, z = b.
+// y[b][k][i] = [x_k (D^_k)^-1]_{d_k} over S source rows at in + b in_bs + koff[k] (moduli
+// mods[mod0 + k]).  Grid: x over coefficients, y = k, z = b.
 __global__ __launch_bounds__(kThreads) void k_modup_scale(const u64* __restrict__ in, u64 in_bs,
-                                                          u32 mod0, u64* __restrict__ y, u32 S,
+                                                          KOff koff, u32 mod0,
+                                                          u64* __restrict__ y, u32 S,
                                                           u32 log_n,
                                                           const ulonglong2* __restrict__ inv,
                                                           const ModParams* __restrict__ mods) {
@@ -211,7 +224,7 @@ __global__ __launch_bounds__(kThreads) void k_modup_scale(const u64* __restrict_
   const u64 q = mods[mod0 + k].q;
   const ulonglong2 w = inv[k];
   y[((u64)b * S + k) * n + i] =
-      csub(shoup_lazy(in[(u64)b * in_bs + (u64)k * n + i], w.x, w.y, q), q);
+      csub(shoup_lazy(in[(u64)b * in_bs + koff.o[k] + i], w.x, w.y, q), q);
 }
 
 // host Shoup-pair table -> device ulonglong2 array (same 16-byte layout)
@@ -227,6 +240,7 @@ int upload(ulonglong2** dptr, const std::vector<Pair64>& v) {
 struct BcArgs {
   const u64* in;
   u64 in_bs;
+  KOff koff;
   u32 src0;
   u64* out;
   u64 out_bs;
@@ -251,7 +265,8 @@ void launch_bc(const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* 
       m.base1 += r0 - m.n0;
       m.n0 = 0;
     }
-    k_baseconv<S, WIDE><<<g, kThreads, 0, s>>>(a.in, a.in_bs, a.src0, a.out + (u64)r0 * n, a.out_bs, t,
+    k_baseconv<S, WIDE><<<g, kThreads, 0, s>>>(a.in, a.in_bs, a.koff, a.src0, a.out + (u64)r0 * n,
+                                               a.out_bs, t,
                                          m, a.skip_lo, a.skip_hi, n, inv, hat, hs, mods);
   }
 }
@@ -335,6 +350,13 @@ size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch) {
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_all,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
                            u32 nlimbs, u32 batch, void* ws, hipStream_t s) {
+  return launch_keyswitch_shard(c, ks0, ks1, CAll::contiguous(c_all, c->L, c->n), d2_own, evk_b,
+                                evk_a, limb0, nlimbs, batch, ws, s);
+}
+
+int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
+                           const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
+                           u32 nlimbs, u32 batch, void* ws, hipStream_t s) {
   if (c->K == 0) {
     set_error("keyswitch: context has no special primes (K = 0)");
     return kInvalid;
@@ -371,10 +393,12 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
   for (u32 j = 0; j < c->dnum; ++j) {
     const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
     u64* e = ext + (u64)j * B * rn;
+    KOff ko{};  // the digit's source rows in c_all
+    for (u32 k = 0; k < hi - lo; ++k) ko.o[k] = call.off(lo + k, n);
     if (fused_up) {
       const u32 S = hi - lo;
       k_modup_scale<<<dim3((u32)(n / kThreads), S, batch), kThreads, 0, s>>>(
-          c_all + (u64)lo * n, (u64)L * n, lo, yws, S, c->log_n, c->d_modup_inv + (size_t)j * alpha,
+          call.ptr, call.bs, ko, lo, yws, S, c->log_n, c->d_modup_inv + (size_t)j * alpha,
           c->d_mods);
       FHE_HIP_CHECK(hipGetLastError());
       // this rank's own rows of digit j are skipped: ks_row_inner takes them from d2_own
@@ -386,7 +410,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
       if ((rc = launch_modup_col(c, ma, s))) return rc;
       continue;
     }
-    const BcArgs up{c_all + (u64)lo * n, (u64)L * n, lo, e, rn, rows, map, lo, hi, batch};
+    const BcArgs up{call.ptr, call.bs, ko, lo, e, rn, rows, map, lo, hi, batch};
     if ((rc = baseconv_any(hi - lo, up, n, c->d_modup_inv + (size_t)j * alpha,
                            c->d_modup_hat + (size_t)j * alpha * M, M, c->d_mods, c->wide, s)))
       return rc;
@@ -440,8 +464,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
     return kOk;
   }
   if ((rc = launch_ntt(c, false, accp, accp, 2 * batch, rn, L, K, s))) return rc;
-  const BcArgs down{accp, rn, L, conv, (u64)nlimbs * n, nlimbs, RowMap{nlimbs, limb0, 0}, 0, 0,
-                    2 * batch};
+  const BcArgs down{accp, rn, rows_contiguous(K, n), L, conv, (u64)nlimbs * n, nlimbs,
+                    RowMap{nlimbs, limb0, 0}, 0, 0, 2 * batch};
   if ((rc = baseconv_any(K, down, n, c->d_moddown_inv, c->d_moddown_hat, M, c->d_mods, c->wide, s)))
     return rc;
   prof_mark(s, "ks_moddown_conv");
@@ -490,7 +514,7 @@ int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u3
       FHE_HIP_CHECK(hipStreamSynchronize(s));  // the host vectors must outlive the copies
     }
   }
-  const BcArgs a{in, 0, s0, out, 0, T, RowMap{T, t0, 0}, 0, 0, 1};
+  const BcArgs a{in, 0, rows_contiguous(S, c->n), s0, out, 0, T, RowMap{T, t0, 0}, 0, 0, 1};
   return baseconv_any(S, a, c->n, d_tab, d_tab + S, M, c->d_mods, c->wide, s);
 }
 

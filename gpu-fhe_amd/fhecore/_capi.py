@@ -47,6 +47,14 @@ SIGNATURES = {
     "fhe_keyswitch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
     "fhe_keyswitch_shard": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp,
                                    _vp]),
+    "fhe_comm_get_unique_id": (_i32, [ctypes.c_char_p]),
+    "fhe_comm_create": (_i32, [ctypes.POINTER(_vp), ctypes.c_char_p, _i32, _i32, _i32]),
+    "fhe_comm_destroy": (_i32, [_vp]),
+    "fhe_comm_shard": (_i32, [_vp, _vp, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
+    "fhe_keyswitch_dist_workspace": (_sz, [_vp, _vp, _u32, _u32]),
+    "fhe_keyswitch_dist": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
+    "fhe_keyswitch_shard_ranked": (_i32, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32,
+                                          _u32, _vp, _vp]),
     "fhe_rescale_workspace": (_sz, [_vp, _u32, _u32]),
     "fhe_rescale": (_i32, [_vp, _vp, _vp, _u32, _u32, _i32, _vp, _vp]),
     "fhe_automorphism": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _i32, _vp]),

@@ -456,15 +456,22 @@ class Context:
                                       None, None, _stream(out)), "fhe_deserialize")
         return out, limb0.value, bool(ntt.value)
 
-    def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0: int, workspace=None):
-        """One rank's key-switch (see fhecore.dist): c_all [..., L, N] coefficient form,
-        d2_own [..., nlimbs, N] NTT form, evk slices [dnum, nlimbs + K, N]."""
+    def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0: int, workspace=None,
+                        ranks: int = None):
+        """One rank's key-switch given the all-gathered coefficient-form d2.
+
+        c_all: [batch, L, N] (ranks=None), or the rank-major all-gather output
+        [ranks, batch, c, N], c = ceil(L / ranks) (fhecore.dist.gather_ranked: no reorder copy);
+        d2_own [batch, nlimbs, N] NTT form of limbs [limb0, limb0 + nlimbs); evk_* [dnum,
+        nlimbs + K, N].  Returns (ks0, ks1) shaped like d2_own."""
         for t, nm in ((c_all, "c_all"), (d2_own, "d2_own"), (evk_b, "evk_b"), (evk_a, "evk_a")):
             _check_tensor(t, nm, (self.n,))
         nl = d2_own.shape[-2]
         batch = d2_own.numel() // (nl * self.n)
-        if c_all.numel() != batch * self.L * self.n:
-            raise ValueError("keyswitch_shard: c_all must be [batch, L, N]")
+        width = self.L if ranks is None else -(-self.L // ranks)
+        if c_all.numel() != (ranks or 1) * batch * width * self.n:
+            raise ValueError("keyswitch_shard: c_all must be [batch, L, N] or "
+                             "[ranks, batch, ceil(L / ranks), N]")
         if tuple(evk_b.shape) != (self.dnum, nl + self.K, self.n) or evk_a.shape != evk_b.shape:
             raise ValueError("keyswitch_shard: evk slices must be [dnum, nlimbs + K, N]")
         ks0, ks1 = _empty_like(d2_own), _empty_like(d2_own)
@@ -472,9 +479,42 @@ class Context:
         ws = workspace if workspace is not None else self.workspace(
             lib.fhe_keyswitch_workspace(self._ptr, nl, batch))
         with torch.cuda.device(self.device):
-            check(lib.fhe_keyswitch_shard(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(c_all),
-                                          _ptr(d2_own), _ptr(evk_b), _ptr(evk_a), limb0, nl,
-                                          batch, _ptr(ws), _stream(d2_own)), "fhe_keyswitch_shard")
+            if ranks is None:
+                check(lib.fhe_keyswitch_shard(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(c_all),
+                                              _ptr(d2_own), _ptr(evk_b), _ptr(evk_a), limb0, nl,
+                                              batch, _ptr(ws), _stream(d2_own)),
+                      "fhe_keyswitch_shard")
+            else:
+                check(lib.fhe_keyswitch_shard_ranked(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(c_all),
+                                                     ranks, _ptr(d2_own), _ptr(evk_b), _ptr(evk_a),
+                                                     limb0, nl, batch, _ptr(ws), _stream(d2_own)),
+                      "fhe_keyswitch_shard_ranked")
+        return ks0, ks1
+
+    def keyswitch_dist(self, comm, d2_own, evk_b, evk_a, chunks: int = 0, workspace=None):
+        """Limb-sharded key-switch over an RCCL communicator, all in libfhecore
+        (fhe_keyswitch_dist): INTT of this rank's limbs, one ncclAllGather per chunk of the batch
+        overlapping the previous chunk's work, then the local key-switch.  comm:
+        fhecore.dist.RcclComm; d2_own [batch, nlimbs, N] NTT form of comm.shard(L)'s limbs;
+        evk_* [dnum, nlimbs + K, N].  Returns (ks0, ks1) shaped like d2_own."""
+        for t, nm in ((d2_own, "d2_own"), (evk_b, "evk_b"), (evk_a, "evk_a")):
+            _check_tensor(t, nm, (self.n,))
+        shard = comm.shard(self.L)
+        nl = d2_own.shape[-2]
+        if nl != shard.nlimbs:
+            raise ValueError(f"keyswitch_dist: d2_own has {nl} limbs, this rank owns "
+                             f"{shard.nlimbs}")
+        batch = d2_own.numel() // (nl * self.n) if nl else d2_own.shape[0]
+        if tuple(evk_b.shape) != (self.dnum, nl + self.K, self.n) or evk_a.shape != evk_b.shape:
+            raise ValueError("keyswitch_dist: evk slices must be [dnum, nlimbs + K, N]")
+        ks0, ks1 = _empty_like(d2_own), _empty_like(d2_own)
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_keyswitch_dist_workspace(self._ptr, comm.handle, batch, chunks))
+        with torch.cuda.device(self.device):
+            check(lib.fhe_keyswitch_dist(self._ptr, comm.handle, _ptr(ks0), _ptr(ks1),
+                                         _ptr(d2_own), _ptr(evk_b), _ptr(evk_a), batch, chunks,
+                                         _ptr(ws), _stream(d2_own)), "fhe_keyswitch_dist")
         return ks0, ks1
 
 

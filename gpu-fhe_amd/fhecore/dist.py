@@ -8,13 +8,22 @@ then finishes ModUp / NTT / inner product / ModDown for its own Q-limbs plus a r
 the K special limbs (so ModDown needs no second collective).  Outputs stay limb-sharded and
 concatenate to the single-device result bit for bit.
 
-The orchestration is written against an "engine" with two methods -- ``intt_(t, limb0)`` and
-``keyswitch_shard(c_all, d2_own, evk_b, evk_a, limb0)``, plus an optional out-of-place
-``intt(t, limb0)`` that saves the copy of d2 -- so fhecore.Context (the HIP path) and a CPU
-restatement used by the gloo tests run the same code.
+Shards: rank r owns Q-limbs [r c, min((r + 1) c, L)), c = ceil(L / G) -- any L and G (the last
+ranks may own fewer limbs, or none).  The all-gather output stays rank-major, [G, batch, c, N]
+with the short blocks padded (gather_ranked), and the key-switch reads that layout directly
+(Context.keyswitch_shard(..., ranks=G)): no reorder copy.
+
+Two drivers run the same algorithm:
+  * sharded_keyswitch -- torch.distributed all-gather + the engine's local step; written against
+    an "engine" (``intt`` / ``intt_`` and ``keyswitch_shard``), so fhecore.Context (HIP) and the
+    CPU restatement of the gloo tests share it;
+  * RcclComm + Context.keyswitch_dist -- the whole exchange inside libfhecore
+    (fhe_keyswitch_dist: its own RCCL communicator and stream, chunked so each chunk's transfer
+    overlaps the previous chunk's key-switch).
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import torch
@@ -30,22 +39,25 @@ class LimbShard:
     rank: int
 
     def __post_init__(self):
-        if self.world < 1 or not 0 <= self.rank < self.world:
+        if self.world < 1 or not 0 <= self.rank < self.world or self.L < 1:
             raise ValueError("bad rank/world")
-        if self.L % self.world:
-            raise ValueError(f"L = {self.L} limbs do not divide evenly over {self.world} ranks")
 
     @property
-    def nlimbs(self) -> int:
-        return self.L // self.world
+    def width(self) -> int:
+        """Limbs per rank block (the last blocks may hold fewer): ceil(L / world)."""
+        return -(-self.L // self.world)
 
     @property
     def lo(self) -> int:
-        return self.rank * self.nlimbs
+        return min(self.L, self.rank * self.width)
 
     @property
     def hi(self) -> int:
-        return self.lo + self.nlimbs
+        return min(self.L, self.lo + self.width)
+
+    @property
+    def nlimbs(self) -> int:
+        return self.hi - self.lo
 
     def own(self, x, limb_dim: int = -2):
         """This rank's slice of a full-limb tensor/array along `limb_dim`."""
@@ -64,20 +76,36 @@ class LimbShard:
         return cls(L, 1, 0)
 
 
-def all_gather_limbs(x_own, shard: LimbShard, group=None):
-    """[..., nlimbs, N] per rank -> [..., L, N] on every rank (rank order = limb order).  One
-    all_gather_into_tensor into a [world, ..., nlimbs, N] buffer, then a limb-major reorder."""
+def gather_ranked(x_own, shard: LimbShard, group=None):
+    """[..., nlimbs, N] per rank -> [world, batch, width, N] on every rank (batch = the flattened
+    leading dims; blocks shorter than `width` padded): one all_gather_into_tensor, no reorder."""
+    n = x_own.shape[-1]
+    lead = 1
+    for d in x_own.shape[:-2]:
+        lead *= d
+    x = x_own.reshape(lead, shard.nlimbs, n)
+    if shard.nlimbs != shard.width:
+        pad = torch.zeros(lead, shard.width, n, dtype=x.dtype, device=x.device)
+        pad[:, :shard.nlimbs] = x
+        x = pad
+    x = x.contiguous()
     if shard.world == 1:
-        return x_own.contiguous()
-    flat = (shard.world * x_own.shape[0],) + tuple(x_own.shape[1:])
-    buf = torch.empty(flat, dtype=x_own.dtype, device=x_own.device)
-    dist.all_gather_into_tensor(buf, x_own.contiguous(), group=group)
-    if x_own.dim() == 2:
-        return buf  # [world * nlimbs, N] is already limb order
-    buf = buf.view((shard.world,) + tuple(x_own.shape))
-    lead = x_own.dim() - 2
-    perm = list(range(1, lead + 1)) + [0, lead + 1, lead + 2]
-    return buf.permute(perm).reshape(tuple(x_own.shape[:-2]) + (shard.L, x_own.shape[-1])).contiguous()
+        return x.reshape(1, lead, shard.width, n)
+    buf = torch.empty((shard.world * lead, shard.width, n), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(buf, x, group=group)
+    return buf.view(shard.world, lead, shard.width, n)
+
+
+def ranked_to_limbs(buf, shard: LimbShard):
+    """[world, batch, width, N] (gather_ranked) -> [batch, L, N] in limb order."""
+    w, lead, width, n = buf.shape
+    return buf.permute(1, 0, 2, 3).reshape(lead, w * width, n)[:, :shard.L].contiguous()
+
+
+def all_gather_limbs(x_own, shard: LimbShard, group=None):
+    """[..., nlimbs, N] per rank -> [..., L, N] on every rank (rank order = limb order)."""
+    full = ranked_to_limbs(gather_ranked(x_own, shard, group), shard)
+    return full.reshape(tuple(x_own.shape[:-2]) + (shard.L, x_own.shape[-1]))
 
 
 def sharded_hommult(engine, a_own, b_own, shard: LimbShard, out=None, workspace=None):
@@ -96,5 +124,54 @@ def sharded_keyswitch(engine, d2_own, evk_b_own, evk_a_own, shard: LimbShard, gr
     else:
         c_own = d2_own.clone()
         engine.intt_(c_own, limb0=shard.lo)
-    c_all = all_gather_limbs(c_own, shard, group)  # the only collective of the whole path
-    return engine.keyswitch_shard(c_all, d2_own, evk_b_own, evk_a_own, shard.lo)
+    c_ranked = gather_ranked(c_own, shard, group)  # the only collective of the whole path
+    return engine.keyswitch_shard(c_ranked, d2_own, evk_b_own, evk_a_own, shard.lo,
+                                  ranks=shard.world)
+
+
+class RcclComm:
+    """libfhecore's own RCCL communicator for fhe_keyswitch_dist (include/fhecore.h).  Rank 0
+    makes the unique id; torch.distributed (any backend) carries it to the others.  One per
+    process/GPU; every rank of `group` must construct it together."""
+
+    def __init__(self, device: int = None, group=None):
+        from ._capi import check, load
+
+        lib = load()
+        if dist.is_available() and dist.is_initialized():
+            self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        else:
+            self.world, self.rank = 1, 0
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            check(lib.fhe_comm_get_unique_id(uid), "fhe_comm_get_unique_id")
+        if self.world > 1:
+            box = [uid.raw if self.rank == 0 else None]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group else 0,
+                                       group=group)
+            uid = ctypes.create_string_buffer(box[0], 128)
+        self._c = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.fhe_comm_create(ctypes.byref(self._c), uid, self.world, self.rank,
+                                      self.device), "fhe_comm_create")
+
+    @property
+    def handle(self):
+        return self._c
+
+    def shard(self, L: int) -> LimbShard:
+        return LimbShard(L, self.world, self.rank)
+
+    def close(self):
+        if getattr(self, "_c", None) and self._c.value:
+            from ._capi import load
+
+            load().fhe_comm_destroy(self._c)
+            self._c = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass

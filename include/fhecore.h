@@ -145,6 +145,37 @@ int fhe_keyswitch_shard(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const 
                         uint32_t limb0, uint32_t nlimbs, uint32_t batch, void* workspace,
                         fhe_stream_t stream);
 
+/* ---- multi-GPU: the limb-sharded key-switch over RCCL ---------------------
+ * One process per GPU.  Rank r of G owns Q-limbs [r c, min((r + 1) c, L)), c = ceil(L / G)
+ * (fhe_comm_shard), plus the K special limbs of the key.  A communicator is created from a
+ * unique id that rank 0 makes (fhe_comm_get_unique_id) and the caller distributes out of band
+ * (e.g. a torch.distributed broadcast), one fhe_comm_create per rank on its device.
+ * fhe_keyswitch_dist: d2_own [batch][nlimbs][N] NTT form of the rank's limbs, evk_b / evk_a
+ * [dnum][nlimbs + K][N] (own Q-limbs then all K P-limbs) -> ks0, ks1 [batch][nlimbs][N] NTT
+ * form.  INTT of the own limbs, one all-gather of the coefficient-form d2 per chunk of the batch
+ * (`chunks` pieces, 0 = default 4; each chunk's transfer runs on the communicator's stream and
+ * overlaps the previous chunk's key-switch), then the local key-switch: the G ranks' outputs
+ * concatenate to fhe_keyswitch's bit for bit.  Every rank must call it with the same batch and
+ * chunks; one call at a time per communicator.
+ * fhe_keyswitch_shard_ranked: the local step alone, on an all-gather output already in the
+ * rank-major layout [ranks][batch][c][N] (blocks of the last ranks padded to c limbs). */
+#define FHE_COMM_ID_BYTES 128
+typedef struct fhe_comm_s* fhe_comm_t;
+int fhe_comm_get_unique_id(uint8_t* id);
+int fhe_comm_create(fhe_comm_t* comm, const uint8_t* id, int nranks, int rank, int device);
+int fhe_comm_destroy(fhe_comm_t comm);
+int fhe_comm_shard(const fhe_ctx* ctx, fhe_comm_t comm, uint32_t* limb0, uint32_t* nlimbs);
+size_t fhe_keyswitch_dist_workspace(const fhe_ctx* ctx, fhe_comm_t comm, uint32_t batch,
+                                    uint32_t chunks);
+int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint64_t* ks1,
+                       const uint64_t* d2_own, const uint64_t* evk_b, const uint64_t* evk_a,
+                       uint32_t batch, uint32_t chunks, void* workspace, fhe_stream_t stream);
+int fhe_keyswitch_shard_ranked(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1,
+                               const uint64_t* c_gathered, uint32_t ranks, const uint64_t* d2_own,
+                               const uint64_t* evk_b, const uint64_t* evk_a, uint32_t limb0,
+                               uint32_t nlimbs, uint32_t batch, void* workspace,
+                               fhe_stream_t stream);
+
 /* ---- rescale and rotation (not in the reference) ---------------------
  * Standard RNS-CKKS operations on this library's layout, restated by oracle/pyoracle.py
  * (rescale_coeff / rescale_ntt, automorphism_*, rotate).

@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -178,6 +179,37 @@ struct Ciphertext {
   uint64_t* data() const { return buf.data(); }
 };
 
+// One rank of a limb-sharded job: libfhecore's RCCL communicator.  Rank 0 calls
+// Comm::unique_id() and sends the bytes to the other ranks (MPI, sockets, torch.distributed...);
+// every rank then constructs its Comm on its own GPU.  shard(ctx) = the Q-limbs this rank owns.
+class Comm {
+ public:
+  using Id = std::array<uint8_t, FHE_COMM_ID_BYTES>;
+  static Id unique_id() {
+    Id id{};
+    check(fhe_comm_get_unique_id(id.data()), "fhe_comm_get_unique_id");
+    return id;
+  }
+  Comm(const Id& id, int nranks, int rank, int device = 0) {
+    check(fhe_comm_create(&c_, id.data(), nranks, rank, device), "fhe_comm_create");
+  }
+  ~Comm() {
+    if (c_) fhe_comm_destroy(c_);
+  }
+  Comm(Comm&& o) noexcept : c_(std::exchange(o.c_, nullptr)) {}
+  Comm(const Comm&) = delete;
+  Comm& operator=(const Comm&) = delete;
+  fhe_comm_t get() const { return c_; }
+  std::pair<uint32_t, uint32_t> shard(const Context& ctx) const {  // (limb0, nlimbs)
+    uint32_t lo = 0, nl = 0;
+    check(fhe_comm_shard(ctx.get(), c_, &lo, &nl), "fhe_comm_shard");
+    return {lo, nl};
+  }
+
+ private:
+  fhe_comm_t c_ = nullptr;
+};
+
 // Homomorphic operations on one stream.
 class Evaluator {
  public:
@@ -227,6 +259,25 @@ class Evaluator {
     check(fhe_keyswitch(ctx_.get(), k0.data(), k1.data(), d2.data(), evk_b.data(), evk_a.data(), 1,
                         ws_.data(), s_),
           "fhe_keyswitch");
+    return {std::move(k0), std::move(k1)};
+  }
+  // The limb-sharded key-switch (fhe_keyswitch_dist): d2_own = this rank's limbs of d2 (NTT
+  // form, comm.shard(ctx) limbs), evk_*_own [dnum][nlimbs + K][N] (own Q-limbs then all P-limbs).
+  // Every rank calls it together; the ranks' outputs concatenate to keyswitch()'s.
+  std::pair<Ciphertext, Ciphertext> keyswitch_dist(const Comm& comm, const Ciphertext& d2_own,
+                                                   const DeviceBuffer& evk_b_own,
+                                                   const DeviceBuffer& evk_a_own,
+                                                   uint32_t chunks = 0) const {
+    if (d2_own.limbs != comm.shard(ctx_).second)
+      throw Error(FHE_EINVAL, "keyswitch_dist: d2_own must hold this rank's limbs");
+    Ciphertext k0(ctx_, d2_own.components, d2_own.limbs, true);
+    Ciphertext k1(ctx_, d2_own.components, d2_own.limbs, true);
+    const size_t need = fhe_keyswitch_dist_workspace(ctx_.get(), comm.get(), d2_own.components, chunks);
+    if (ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
+    check(fhe_keyswitch_dist(ctx_.get(), comm.get(), k0.data(), k1.data(), d2_own.data(),
+                             evk_b_own.data(), evk_a_own.data(), d2_own.components, chunks,
+                             ws_.data(), s_),
+          "fhe_keyswitch_dist");
     return {std::move(k0), std::move(k1)};
   }
   // Public-key encryption of an NTT-form plaintext (1 component, L limbs) -> [2][L][N] NTT form.

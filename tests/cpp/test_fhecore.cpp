@@ -148,6 +148,44 @@ int main() {
         return 1;
       }
     }
+    {  // the limb-sharded key-switch over a one-rank RCCL communicator == fhe_keyswitch
+      fhe::Context kc = fhe::Context::standard(log_n, 4, 2, 2);
+      const fhe::Comm comm(fhe::Comm::unique_id(), 1, 0, 0);
+      const auto sh = comm.shard(kc);
+      std::vector<u64> mq(6);
+      fhe::check(fhe_ctx_moduli(kc.get(), mq.data(), nullptr), "moduli");
+      const uint32_t B = 3;
+      fhe::Ciphertext d2(kc, B, 4, true);
+      std::vector<u64> hd2((size_t)B * 4 * n);
+      for (size_t i = 0; i < hd2.size(); ++i) hd2[i] = rng() % mq[(i / n) % 4];
+      d2.buf.upload(hd2);
+      fhe::DeviceBuffer eb((size_t)2 * 6 * n), ea((size_t)2 * 6 * n);
+      std::vector<u64> he(2 * 6 * n), ha2(2 * 6 * n);
+      for (size_t i = 0; i < he.size(); ++i) {
+        he[i] = rng() % mq[(i / n) % 6];
+        ha2[i] = rng() % mq[(i / n) % 6];
+      }
+      eb.upload(he);
+      ea.upload(ha2);
+      fhe::Evaluator kev(kc);
+      const auto dist = kev.keyswitch_dist(comm, d2, eb, ea, 2);
+      const auto r0 = dist.first.buf.download(), r1 = dist.second.buf.download();
+      for (uint32_t b = 0; b < B; ++b) {
+        fhe::Ciphertext one(kc, 1, 4, true);
+        one.buf.upload(std::vector<u64>(hd2.begin() + (size_t)b * 4 * n, hd2.begin() + (size_t)(b + 1) * 4 * n));
+        const auto ref = kev.keyswitch(one, eb, ea);
+        const auto f0 = ref.first.buf.download(), f1 = ref.second.buf.download();
+        for (u64 i = 0; i < 4 * n; ++i)
+          if (r0[b * 4 * n + i] != f0[i] || r1[b * 4 * n + i] != f1[i]) {
+            std::printf("FAIL keyswitch_dist ct %u word %llu\n", b, (unsigned long long)i);
+            return 1;
+          }
+      }
+      if (sh.first != 0 || sh.second != 4) {
+        std::printf("FAIL comm shard\n");
+        return 1;
+      }
+    }
     std::printf("cpp api ok\n");
     return 0;
   } catch (const fhe::Error& e) {

@@ -12,7 +12,8 @@ import torch.multiprocessing as mp
 
 import coracle
 import pyoracle
-from fhecore.dist import LimbShard, all_gather_limbs, sharded_hommult, sharded_keyswitch
+from fhecore.dist import (LimbShard, all_gather_limbs, ranked_to_limbs, sharded_hommult,
+                          sharded_keyswitch)
 
 LOG_N, L, K, DNUM = 6, 4, 2, 2
 
@@ -33,15 +34,23 @@ class CpuEngine:
 
     def intt_(self, t, limb0=0):
         nl = t.shape[-2]
+        if nl == 0:
+            return t
         t.copy_(_t(coracle.ntt_inv(_a(t), self.qs[limb0:limb0 + nl])))
         return t
 
     def hommult(self, a, b, out=None, limb0=0, workspace=None):
         nl = a.shape[-2]
+        if nl == 0:  # a rank without limbs (uneven shards)
+            return torch.empty(a.shape[:-3] + (3, 0, a.shape[-1]), dtype=torch.int64)
         return _t(coracle.hommult(_a(a), _a(b), self.qs[limb0:limb0 + nl]))
 
-    def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0):
+    def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0, ranks=None):
         nl = d2_own.shape[-2]
+        if nl == 0:
+            return torch.empty_like(d2_own), torch.empty_like(d2_own)
+        if ranks is not None:  # the rank-major all-gather output [ranks, batch, width, N]
+            c_all = ranked_to_limbs(c_all, LimbShard(L, ranks, 0))
         ca, da = _a(c_all).reshape(-1, L, 1 << LOG_N), _a(d2_own).reshape(-1, nl, 1 << LOG_N)
         outs = [pyoracle.keyswitch_shard(c, d, _a(evk_b), _a(evk_a), self.qs, self.ps, DNUM, limb0,
                                          limb0 + nl) for c, d in zip(ca, da)]
@@ -77,10 +86,9 @@ def _worker(rank, world, port, q):
                             shard)
         g0 = all_gather_limbs(k0, shard)
         g1 = all_gather_limbs(k1, shard)
-        dd = [torch.empty_like(d) for _ in range(world)]
-        dist.all_gather(dd, d)
+        gd = all_gather_limbs(d, shard)
         if rank == 0:
-            q.put((_a(g0).copy(), _a(g1).copy(), np.concatenate([_a(x) for x in dd], axis=2)))
+            q.put((_a(g0).copy(), _a(g1).copy(), _a(gd).copy()))
     finally:
         dist.destroy_process_group()
 
@@ -91,8 +99,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_keyswitch_and_hommult_gloo(world):
+    """world 3 over L = 4 limbs: uneven shards (2, 2, 0 limbs; the idle rank still joins the
+    all-gather with a padded block)."""
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
@@ -112,12 +122,32 @@ def test_sharded_keyswitch_and_hommult_gloo(world):
 
 def test_limb_shard_ranges():
     s = LimbShard(16, 8, 3)
-    assert (s.lo, s.hi, s.nlimbs) == (6, 8, 2)
+    assert (s.lo, s.hi, s.nlimbs, s.width) == (6, 8, 2, 2)
     assert s.evk_rows(4) == [6, 7, 16, 17, 18, 19]
+    # uneven: ceil(L / G) per rank, the remainder on the last ranks
+    assert [(LimbShard(10, 4, r).lo, LimbShard(10, 4, r).nlimbs) for r in range(4)] == \
+        [(0, 3), (3, 3), (6, 3), (9, 1)]
+    assert [LimbShard(10, 8, r).nlimbs for r in range(8)] == [2, 2, 2, 2, 2, 0, 0, 0]
     with pytest.raises(ValueError):
-        LimbShard(10, 4, 0)
+        LimbShard(10, 4, 4)
     x = torch.arange(16 * 3).reshape(16, 3)
     assert s.own(x).tolist() == x[6:8].tolist()
+
+
+def test_ranked_layout_round_trip():
+    """Rank-major padded blocks (what gather_ranked's all-gather produces) map back to limb
+    order exactly, for even and uneven shards; a single rank's gather is its padded block."""
+    from fhecore.dist import gather_ranked
+
+    x = torch.arange(2 * 10 * 4).reshape(2, 10, 4)
+    assert (gather_ranked(x, LimbShard(10, 1, 0)) == x[None]).all()
+    for world in (2, 3, 4, 8):
+        sh0 = LimbShard(10, world, 0)
+        buf = torch.zeros(world, 2, sh0.width, 4, dtype=x.dtype)
+        for r in range(world):  # single-process emulation of the all-gather
+            sh = LimbShard(10, world, r)
+            buf[r, :, :sh.nlimbs] = sh.own(x)
+        assert (ranked_to_limbs(buf, sh0) == x).all()
 
 
 def test_single_rank_shard_is_identity():

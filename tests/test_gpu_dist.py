@@ -1,0 +1,93 @@
+"""GPU tests of the native multi-GPU key-switch (gpu-fhe_amd/csrc/dist.cpp):
+the rank-major all-gather layout that the local key-switch reads without a reorder copy (every
+rank of an even or uneven G-way sharding, run one after another on this GPU), and the full
+fhe_keyswitch_dist path over a one-rank RCCL communicator (INTT + ncclAllGather + key-switch, in
+chunks) -- all bit-exact against the single-device key-switch and the C oracle.  Multi-rank
+orchestration runs over gloo on the CPU (tests/test_dist_cpu.py); N > 1 GPUs are not available to
+these tests."""
+import numpy as np
+import pytest
+
+import coracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fc():
+    import fhecore
+
+    return fhecore
+
+
+def rand(mods, log_n, lead=(), seed=0):
+    rng = np.random.default_rng(seed)
+    n = 1 << log_n
+    return np.stack([rng.integers(0, q, size=lead + (n,), dtype=np.uint64) for q in mods],
+                    axis=len(lead))
+
+
+@pytest.mark.parametrize("log_n,L,K,dnum,G,batch", [
+    (16, 16, 4, 4, 8, 2),   # configs[3]: 2 limbs per rank, the fused kernels
+    (12, 16, 4, 4, 6, 3),   # uneven: 3,3,3,3,3,1 limbs
+    (12, 10, 2, 2, 4, 2),   # uneven digits and shards: 3,3,3,1
+    (12, 10, 2, 3, 8, 1),   # ranks without limbs: 2,2,2,2,2,0,0,0
+])
+def test_ranked_gather_layout_shards(fc, log_n, L, K, dnum, G, batch):
+    from fhecore.dist import LimbShard
+
+    ctx = fc.Context(log_n, L=L, K=K, dnum=dnum)
+    d2 = rand(ctx.moduli, log_n, (batch,), seed=L + G)
+    eb = rand(ctx.all_moduli, log_n, (dnum,), seed=1)
+    ea = rand(ctx.all_moduli, log_n, (dnum,), seed=2)
+    full0, full1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(eb), fc.to_device(ea))
+    c = coracle.ntt_inv(d2, ctx.moduli)  # coefficient form of every limb
+    width = -(-L // G)
+    ranked = np.zeros((G, batch, width, 1 << log_n), dtype=np.uint64)
+    for r in range(G):  # what the all-gather leaves on every rank
+        sh = LimbShard(L, G, r)
+        ranked[r, :, :sh.nlimbs] = c[:, sh.lo:sh.hi]
+    ranked_d = fc.to_device(ranked)
+    parts0, parts1 = [], []
+    for r in range(G):
+        sh = LimbShard(L, G, r)
+        if sh.nlimbs == 0:
+            continue
+        rows = sh.evk_rows(K)
+        k0, k1 = ctx.keyswitch_shard(ranked_d, fc.to_device(np.ascontiguousarray(d2[:, sh.lo:sh.hi])),
+                                     fc.to_device(np.ascontiguousarray(eb[:, rows])),
+                                     fc.to_device(np.ascontiguousarray(ea[:, rows])), sh.lo,
+                                     ranks=G)
+        parts0.append(fc.to_host(k0))
+        parts1.append(fc.to_host(k1))
+    assert (np.concatenate(parts0, axis=1) == fc.to_host(full0)).all()
+    assert (np.concatenate(parts1, axis=1) == fc.to_host(full1)).all()
+    # a window that is not a rank's shard is refused
+    with pytest.raises(fc.FheError):
+        ctx.keyswitch_shard(ranked_d, fc.to_device(np.ascontiguousarray(d2[:, 1:2])),
+                            fc.to_device(np.ascontiguousarray(eb[:, [1] + list(range(L, L + K))])),
+                            fc.to_device(np.ascontiguousarray(ea[:, [1] + list(range(L, L + K))])),
+                            1, ranks=G)
+
+
+@pytest.mark.parametrize("batch,chunks", [(1, 0), (4, 0), (5, 4), (3, 8), (6, 2)])
+def test_keyswitch_dist_one_rank_rccl(fc, batch, chunks):
+    """fhe_keyswitch_dist through a real RCCL communicator (world 1): INTT into the gather buffer,
+    ncclAllGather on the communicator's stream, chunked key-switch; equals fhe_keyswitch and the
+    oracle."""
+    from fhecore.dist import RcclComm
+
+    L, K, dnum, log_n = 16, 4, 4, 14
+    ctx = fc.Context(log_n, L=L, K=K, dnum=dnum)
+    comm = RcclComm()
+    assert (comm.world, comm.rank) == (1, 0) and comm.shard(L).nlimbs == L
+    d2 = rand(ctx.moduli, log_n, (batch,), seed=batch)
+    eb = rand(ctx.all_moduli, log_n, (dnum,), seed=3)
+    ea = rand(ctx.all_moduli, log_n, (dnum,), seed=4)
+    k0, k1 = ctx.keyswitch_dist(comm, fc.to_device(d2), fc.to_device(eb), fc.to_device(ea),
+                                chunks=chunks)
+    r0, r1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(eb), fc.to_device(ea))
+    assert (fc.to_host(k0) == fc.to_host(r0)).all() and (fc.to_host(k1) == fc.to_host(r1)).all()
+    o0, o1 = coracle.keyswitch(d2[0], eb, ea, ctx.moduli, ctx.special, dnum)
+    assert (fc.to_host(k0)[0] == o0).all() and (fc.to_host(k1)[0] == o1).all()
+    comm.close()
