@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--bits", type=int, default=60, choices=[60, 61, 62, 63],
                     help="hommult: modulus chain of the largest primes below 2^bits (62, 63: the "
                          "exact wide-modulus butterflies)")
+    ap.add_argument("--ks-chunks", type=int, default=0,
+                    help="keyswitch: all-gather chunks per batch (0 = 1 at N = 1, 4 above)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -447,18 +449,15 @@ def run_keyswitch(args, world, rank):
     evk_a = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
     B = args.batch
     d2 = uniform_limbs(gen, ctx.moduli[shard.lo:shard.hi], (B,), n)
-    ws = ctx.workspace(load().fhe_keyswitch_workspace(ctx.handle, shard.nlimbs, B))
-
-    class Eng:  # the Context, with a preallocated workspace
-        intt_ = ctx.intt_
-        intt = ctx.intt
-
-        @staticmethod
-        def keyswitch_shard(c_all, d2_own, eb, ea, limb0):
-            return ctx.keyswitch_shard(c_all, d2_own, eb, ea, limb0, workspace=ws)
+    # the native path: libfhecore's RCCL communicator, INTT + all-gather + key-switch in
+    # fhe_keyswitch_dist, chunked so a chunk's transfer overlaps the previous chunk's work (one
+    # chunk at N = 1: nothing to overlap, and a whole batch reads the key once)
+    comm = fdist.RcclComm()
+    chunks = args.ks_chunks or (1 if world == 1 else 4)
+    ws = ctx.workspace(load().fhe_keyswitch_dist_workspace(ctx.handle, comm.handle, B, chunks))
 
     def step():
-        fdist.sharded_keyswitch(Eng, d2, evk_b, evk_a, shard)
+        ctx.keyswitch_dist(comm, d2, evk_b, evk_a, chunks=chunks, workspace=ws)
 
     dt, kavg = timed(step, args, world, 64 * args.steps + 64)
     ks_per_s = B * args.steps / dt
@@ -470,8 +469,9 @@ def run_keyswitch(args, world, rank):
     out = {"metric": "key-switches/sec at N=2^16, L=16, K=4, dnum=4 (RNS limbs sharded, RCCL all-gather)",
            "value": round(ks_per_s, 2), "unit": "keyswitch/s",
            "ms_per_step": round(dt / args.steps * 1e3, 4),
-           "config": {"workload": "hybrid key-switch, BASELINE configs[3]", "log_n": args.log_n,
-                      "L": L, "K": K, "dnum": dnum, "batch": B, "parallelism": f"rns-limb-shard x{world}"},
+           "config": {"workload": "hybrid key-switch, BASELINE configs[3] (fhe_keyswitch_dist)",
+                      "log_n": args.log_n, "L": L, "K": K, "dnum": dnum, "batch": B,
+                      "chunks": chunks, "parallelism": f"rns-limb-shard x{world}"},
            "keyswitch_alg_hbm_gbps_per_gpu": round(gbps, 1),
            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
            "roofline": roofline("keyswitch (whole, per GPU)", alg // world, dt / (B * args.steps) * 1e3,
@@ -521,6 +521,11 @@ def run_mulrelin(args, world, rank):
 
 
 def main():
+    # stdout carries exactly one JSON line: anything else the libraries print there (RCCL prints
+    # its version banner to stdout when a communicator comes up) is sent to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     args = parse()
     if args.batch is None:
         args.batch = 64 if args.workload == "hommult" else 16
@@ -538,7 +543,8 @@ def main():
                 "config": out.pop("config")}
         line.update(out)
         line["cpu_baseline"] = cpu
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     if world > 1:
         torch.distributed.destroy_process_group()
 
