@@ -111,9 +111,6 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
 int ctx_destroy(fhe_ctx* c) {
   if (!c) return kOk;
   (void)hipSetDevice(c->device);
-  if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
-  if (c->aux_fork) (void)hipEventDestroy(c->aux_fork);
-  if (c->aux_join) (void)hipEventDestroy(c->aux_join);
   for (auto& t : c->bc_tables) (void)hipFree(t.second);
   for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_inv, (void*)c->d_nfold, (void*)c->d_nfold_down,
                     (void*)c->d_modup_inv, (void*)c->d_modup_hat, (void*)c->d_moddown_inv,

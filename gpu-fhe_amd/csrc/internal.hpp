@@ -72,10 +72,6 @@ struct fhe_ctx {
   // built on first use (rns.hip launch_baseconv) and freed with the context
   std::mutex bc_mutex;
   std::vector<std::pair<uint64_t, ulonglong2*>> bc_tables;
-  // helper stream for split-batch HomMult (created on first use; fork/join by events)
-  hipStream_t aux_stream = nullptr;
-  hipEvent_t aux_fork = nullptr, aux_join = nullptr;
-  std::mutex aux_mutex;
 };
 
 namespace fhe {

@@ -14,12 +14,12 @@
 // Inside a pass, each thread holds E = 16 elements of one sub-transform in VGPRs and runs up to
 // 4 butterfly stages per LDS round trip (radix-16 rounds); twiddles come from the per-limb
 // table psi^brv (16-byte {w, floor(w 2^64 / q)} Shoup pairs, L2-resident).  Butterflies are
-// lazy (FHE_BFLY below): forward values live in [0, 8q), inverse in [0, 3q) between stages and
+// lazy (round_compute): forward values live below H q, inverse in [0, 3q) between stages and
 // passes; the last pass reduces to [0, q).
 //
-// HomMult (config 3) = 4 launches: column-forward on a, then on b -> one fused row kernel
+// HomMult (config 3) = 3 launches: column-forward of a and b's 4 polys -> one fused row kernel
 // (row-forward x4, tensor d0 = A0B0, d1 = A0B1 + A1B0, d2 = A1B1 in LDS, row-inverse x3) ->
-// column-inverse on the 3 output polys.
+// column-inverse on the 3 output polys.  Moduli of 61-63 bits take exact butterflies (H = 2).
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -37,68 +37,26 @@ namespace {
 constexpr int kElog = 4;
 constexpr int kE = 1 << kElog;
 constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per workgroup
-// FHE_COL_THREADS: column-pass workgroup size; more threads = wider tiles (16 columns per 256
-// threads at N = 2^16), i.e. longer contiguous runs per row in HBM, at the same LDS per wave.
-// 512 measured: ntt-batch (N = 2^17) column pass -4 %, HomMult column inverse +9 %; 256 kept.
-#ifndef FHE_COL_THREADS
-#define FHE_COL_THREADS kThreads
-#endif
-constexpr int kColThreads = FHE_COL_THREADS;
-// FHE_NTT_ABLATE (timing-only A/B builds, tools/build_variant.sh; never the shipped library):
-// 1 = skip the butterflies of the generic passes, 2 = skip their global loads/stores,
-// 3 = row passes read row 0's twiddles for every row (wrong results; twiddle-fetch cost).
-#ifndef FHE_NTT_ABLATE
-#define FHE_NTT_ABLATE 0
-#endif
-// FHE_BFLY selects the butterfly arithmetic:
-//  0  Harvey with exact Shoup (forward values in [0, 4q), inverse in [0, 2q));
-//  1  the same through the instruction-shaped helpers of modarith.hpp (wins 20 % in the
-//     register-only microbenchmark tools/microbench/bfly_rate.hip, ties inside the kernels);
-//  2  Shoup with the 3-product quotient estimate (shoup_q3, products in [0, 3q)) and wider lazy
-//     ranges: forward values in [0, 8q) (u = x mod 4q, outputs u + t and u - t + 3q), inverse in
-//     [0, 3q) (sum mod 3q, (u - v + 3q) w).  Needs 8q < 2^64, i.e. q < 2^61 (ctx_create checks).
-#ifndef FHE_BFLY
-#define FHE_BFLY 2
-#endif
-// FHE_FOLD_U: the forward CT butterfly folds its X-operand into the product's remainder chain
-// (shoup_q3_add): one 64-bit add fewer per butterfly.
-#ifndef FHE_FOLD_U
-#define FHE_FOLD_U 1
-#endif
-#ifndef FHE_HM_POLY_MAJOR
-#define FHE_HM_POLY_MAJOR 1
-#endif
-// FHE_NTT_MAX_WAVES: occupancy the register allocator / scheduler may assume (waves per SIMD).
-// LDS already caps these kernels at 4 workgroups per CU, so a lower target costs no waves and
-// lets the scheduler spend VGPRs on interleaving independent butterflies.
-#ifndef FHE_NTT_MAX_WAVES
-#define FHE_NTT_MAX_WAVES 8
-#endif
-// ... and the occupancy they must keep: LDS allows 4 workgroups (16 waves) per CU, so anything
-// above 128 VGPRs would cost waves; the item loops' prefetch registers must fit under that.
-#ifndef FHE_NTT_MIN_WAVES
-#define FHE_NTT_MIN_WAVES 4
-#endif
-// FHE_ITEM_LOOP bit 0: column passes, bit 1: row passes run one-generation grids whose
-// workgroups loop over items, prefetching the next one (else one workgroup per item).
-#ifndef FHE_ITEM_LOOP
-#define FHE_ITEM_LOOP 0
-#endif
-constexpr bool kLoopCol = (FHE_ITEM_LOOP & 1) != 0, kLoopRow = (FHE_ITEM_LOOP & 2) != 0;
-// FHE_ROW_XOUT: forward row passes (k_ntt_row, k_moddown_row) store their last round in linear
-// order through the LDS (pass_run XOUT): ntt-batch row-forward 20.7 -> 19.0 ms, ModDown finish
-// 255 -> 190 us.  FHE_ROW_XIN: the inverse row pass loads its first round the same way: row
-// inverse 121.5 -> 118.3 us at E = 16 (it was 3.5 % slower at E = 8, where the partial-line loads
-// were L1 hits).
-#ifndef FHE_ROW_XOUT
-#define FHE_ROW_XOUT 1
-#endif
-#ifndef FHE_ROW_XIN
-#define FHE_ROW_XIN 1
-#endif
-constexpr bool kRowXout = FHE_ROW_XOUT != 0, kRowXin = FHE_ROW_XIN != 0;
+// Column-pass workgroup size: 16 columns per 256 threads at N = 2^16.  (512 threads, i.e. wider
+// tiles, measured -4 % on the N = 2^17 ntt-batch column pass and +9 % on the HomMult column
+// inverse; 256 kept everywhere.)
+constexpr int kColThreads = kThreads;
+// Occupancy the register allocator / scheduler may assume (waves per SIMD): LDS caps these kernels
+// at 4 workgroups (16 waves) per CU, so a lower target costs no waves and lets the scheduler spend
+// VGPRs on interleaving independent butterflies; anything above 128 VGPRs would cost waves.
 #define FHE_KATTR \
-  __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES)))
+  __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
+
+// Butterfly arithmetic (measured choices; DESIGN.md §3, §8 keep the alternatives' numbers):
+//  * Shoup with the 3-product quotient estimate (shoup_q3, products in [0, 3q)) and lazy ranges:
+//    forward values below H q (fwd_range), inverse in [0, 3q) (sum mod 3q, (u - v + 3q) w).  Needs
+//    8q < 2^64, i.e. q < 2^61; wider moduli take the exact H = 2 form;
+//  * the forward CT butterfly folds its X-operand into the product's remainder chain
+//    (shoup_q3_add): one 64-bit add fewer per butterfly;
+//  * conditional subtractions by sign-mask select (csub_fast);
+//  * the forward row passes store their last round in linear order through the LDS (pass_run
+//    XOUT: ntt-batch row-forward 20.7 -> 19.0 ms, ModDown finish 255 -> 190 us) and the inverse
+//    row pass loads its first round the same way (121.5 -> 118.3 us).
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -161,11 +119,6 @@ struct Layout {
   }
 };
 
-// FHE_FINAL_TOPBITS: the final forward reduction's one-step estimate for moduli just below 2^60
-// (round_compute).
-#ifndef FHE_FINAL_TOPBITS
-#define FHE_FINAL_TOPBITS 1
-#endif
 // kFinalFwd reduces the last forward stage to [0, q); kFinalFwd2 only to [0, 2q) (the fused
 // HomMult tensor: its Montgomery products accept operands below 2q).
 enum Final : int { kNotFinal = 0, kFinalFwd = 1, kFinalInv = 2, kFinalFwd2 = 3 };
@@ -270,29 +223,18 @@ __device__ __forceinline__ ulonglong2 ld_tw(const ulonglong2* p) {
   return make_ulonglong2(v.x, v.y);
 }
 
-// Conditional subtraction in the butterflies.  FHE_CSUB_FAST = 1: sign-mask select (csub_fast:
-// one 64-bit add, an arithmetic shift and two v_bfi, no VCC) instead of a 64-bit compare, two
-// v_cndmask and a borrow chain.  Needs |x - m| < 2^63, which every lazy range here satisfies.
-#ifndef FHE_CSUB_FAST
-#define FHE_CSUB_FAST 1
-#endif
+// Conditional subtraction in the butterflies: sign-mask select (csub_fast: one 64-bit add, an
+// arithmetic shift and two v_bfi, no VCC) instead of a 64-bit compare, two v_cndmask and a borrow
+// chain.  Needs |x - m| < 2^63, which every range here satisfies.
 __device__ __forceinline__ u64 csubk(u64 x, u64 m) {
-#if FHE_CSUB_FAST
   // -m as an opaque uniform: otherwise x + (0 - m) folds back into a borrow chain (sub_co/subb,
   // two instructions) instead of one v_lshl_add_u64
   u64 nm = 0 - m;
   asm("" : "+s"(nm));
   return csub_fast(x, nm);
-#else
-  return csub(x, m);
-#endif
 }
 
-struct NoHook {
-  __device__ __forceinline__ void operator()() const {}
-};
-
-// Forward lazy ranges (FHE_BFLY = 2), in units of q.  A CT stage maps X-operands below r q to
+// Forward lazy ranges, in units of q.  A CT stage maps X-operands below r q to
 // outputs below (r' + 3) q, where r' = r unless r + 3 would exceed the headroom H (values must stay
 // below H q <= 2^64), in which case X is first reduced by H/2 q (r' = H/2).  H = 16 needs q < 2^60
 // and subtracts at about every other stage; H = 8 (q < 2^61) at every stage once warm.
@@ -306,20 +248,18 @@ constexpr int fwd_range(int r0, int stages, int H) {
 // Runs one round's butterfly stages on the 16 values a thread holds in registers.
 // Element j sits at sub-transform position tp | Lay::jpos(j).  `base` selects the twiddle rows:
 // local stage st, group g reads tw[(base << st) + g] (base = 1 for the column pass, R1 + row for
-// the row pass).  All of the round's twiddle loads are issued first; then `hook` runs (after a
-// compiler memory fence, so its global loads queue behind the twiddles and waiting for a twiddle
-// never waits for them: vmcnt retires in issue order).
+// the row pass).
 // GATHER = false leaves the twiddle loads to the scheduler, next to their butterflies (better for
 // the column pass, whose twiddles are few and shared); true issues them all first (the row passes:
 // per-lane twiddles from L2, whose latency then overlaps instead of stalling each stage).
 // ROWTAB: the twiddles come from a row table region (base = R1 + row), whose low-bit-round stages
 // are stored lane-major.
 template <int LOGR, int KB, int LO, bool FWD, int FIN, bool GATHER = false, int H = 8,
-          int RIN = 8, bool ROWTAB = GATHER, class Hook = NoHook>
+          int RIN = 8, bool ROWTAB = GATHER>
 __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
                                               const ulonglong2* __restrict__ tw, const u32 base,
                                               const u64 q, const ulonglong2 nf0,
-                                              const ulonglong2 nf1, const Hook& hook = Hook{}) {
+                                              const ulonglong2 nf1) {
   using Lay = Layout<LOGR, KB, LO>;
   using TS = TwSlots<LOGR, KB, LO>;
   constexpr int E = Lay::E;
@@ -332,7 +272,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       constexpr int st = LOGR - 1 - bitpos;
       if constexpr (!(FIN == kFinalInv && st == 0)) {  // the last inverse stage folds N^-1 instead
         // natural group index: g = t W + sj, W = 2^(kElog - bitpos - 1) (the low-bit round has
-        // tp = t << kElog); the row tables store those stages lane-major (context.cpp
+        // tp = t << kElog); the row tables store those stages lane-major (host_tables.cpp
         // lane_major_rows), so the load index is sj TPS + t and a wavefront reads contiguous words
         const u32 sj = Lay::jpos(TS::T.rep_j[sl]) >> (bitpos + 1);
         const u32 g = (ROWTAB && LO == 0) ? sj * ((1u << LOGR) / E) + (tp >> kElog)
@@ -342,7 +282,6 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
     });
     asm volatile("" ::: "memory");
   }
-  hook();
   static_assert(GATHER || !(ROWTAB && LO == 0), "lane-major row twiddles are gathered");
   auto twiddle = [&](int b, int j, int bitpos, int st) {
     if constexpr (GATHER) return tws[TS::T.slot[b][j]];
@@ -350,10 +289,8 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
     return ld_tw(tw + (base << st) + g);
   };
   const u64 q2 = 2 * q, nq = 0 - q;
-  [[maybe_unused]] const u64 nq2 = 0 - q2, q2p1 = q2 + 1;
   // 3q as an opaque uniform: otherwise u + 3q is strength-reduced into a mad per butterfly
-  [[maybe_unused]] u64 q3 = 3 * q;
-  [[maybe_unused]] const u64 q4 = 4 * q;
+  u64 q3 = 3 * q;
   asm("" : "+s"(q3));
   if constexpr (FWD && H == 2) {
     // wide moduli (2^61 <= q < 2^63, ctx->wide): no lazy headroom.  Values stay below 2q:
@@ -379,10 +316,9 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       for (int j = 0; j < E; ++j) x[j] = csubk(x[j], q);
     }
   } else if constexpr (FWD) {
-#if FHE_BFLY == 2
     // CT: X-operands below r q (the static range of this stage, fwd_range), reduced by H/2 q
     // only when the stage would outgrow H q; v = w x[jj] in [0, 3q); outputs below (r' + 3) q
-    [[maybe_unused]] const u64 qh = (u64)(H / 2) * q;
+    const u64 qh = (u64)(H / 2) * q;
     static_for<0, KB>([&](auto sc) {
       constexpr int done = decltype(sc)::value;
       constexpr int b = KB - 1 - done;
@@ -395,7 +331,6 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
         const ulonglong2 w = twiddle(b, j, bitpos, st);
-#if FHE_FOLD_U
         u64 u = reduce ? csubk(x[j], qh) : x[j];
         FHE_OPAQUE(u);  // keeps 2u + 3q one v_lshl_add_u64 (not distributed over the select)
         // u + v straight out of the remainder chain; u - v + 3q = (2u + 3q) - (u + v)
@@ -405,12 +340,6 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         u64 t2 = (u << 1) + q3;
         FHE_OPAQUE(t2);
         x[jj] = t2 - s;
-#else
-        const u64 u = reduce ? csubk(x[j], qh) : x[j];
-        const u64 v = shoup_q3(x[jj], w.x, w.y, nq);
-        x[j] = u + v;
-        x[jj] = u - v + q3;
-#endif
       }
     });
     if constexpr (FIN == kFinalFwd || FIN == kFinalFwd2) {
@@ -420,8 +349,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       // q in [2^60 - 2^56, 2^60) (wave-uniform test; the default moduli are the largest primes
       // below 2^60): x - (x >> 60) q < 2q for any x < 16 q, one estimate instead of up to three
       // halving steps (k = x >> 60 <= x / q, and x - k q < x (2^60 - q) / 2^60 + q < 2q)
-      if (FHE_FINAL_TOPBITS && rout > 4 && rout <= 16 && (q >> 56) == 15) {
-        const u64 nq = 0 - q;
+      if (rout > 4 && rout <= 16 && (q >> 56) == 15) {
 #pragma unroll
         for (int j = 0; j < E; ++j) {
           x[j] += (u64)(u32)(x[j] >> 60) * nq;  // x - k q (mod 2^64, exact: the result is >= 0)
@@ -437,38 +365,6 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         }
       }
     }
-#else
-#pragma unroll
-    for (int b = KB - 1; b >= 0; --b) {
-      const int bitpos = LO + b;
-      const int st = LOGR - 1 - bitpos;
-#pragma unroll
-      for (int j = 0; j < E; ++j) {
-        if (j & (1 << b)) continue;
-        const int jj = j | (1 << b);
-        const ulonglong2 w = twiddle(b, j, bitpos, st);
-#if FHE_BFLY == 1
-        const u64 u = csub_fast(x[j], nq2);
-        const u64 v = shoup_fast(x[jj], w.x, w.y, nq);
-        x[j] = u + v;
-        x[jj] = sub_plus(u, v, q2p1);
-#else
-        // Harvey CT: u in [0, 4q) -> [0, 2q); v = w x[jj] in [0, 2q); outputs in [0, 4q)
-        const u64 u = csub(x[j], q2);
-        const u64 v = shoup_lazy(x[jj], w.x, w.y, q);
-        x[j] = u + v;
-        x[jj] = u - v + q2;
-#endif
-      }
-    }
-    if constexpr (FIN == kFinalFwd || FIN == kFinalFwd2) {
-#pragma unroll
-      for (int j = 0; j < E; ++j) {
-        x[j] = csub(x[j], q2);
-        if constexpr (FIN == kFinalFwd) x[j] = csub(x[j], q);
-      }
-    }
-#endif
   } else if constexpr (H == 2) {
     // wide GS: canonical inputs; sum mod q, (u - v + q) w by the exact Shoup product, reduced
     static_for<0, KB>([&](auto bc) {
@@ -492,6 +388,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       }
     });
   } else {
+    // GS: inputs in [0, 3q); sum -> [0, 3q); (u - v + 3q) w -> [0, 3q)
 #pragma unroll
     for (int b = 0; b < KB; ++b) {
       const int bitpos = LO + b;
@@ -501,36 +398,15 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
         const u64 u = x[j], v = x[jj];
-#if FHE_BFLY == 2
-        // GS: inputs in [0, 3q); sum -> [0, 3q); (u - v + 3q) w -> [0, 3q)
         const u64 sum = u + v, dif = u - v + q3;
-#elif FHE_BFLY == 1
-        const u64 sum = u + v, dif = sub_plus(u, v, q2p1);
-#else
-        // Harvey GS: inputs in [0, 2q); sum -> [0, 2q); (u - v + 2q) w -> [0, 2q)
-        const u64 sum = u + v, dif = u - v + q2;
-#endif
         if (FIN == kFinalInv && st == 0) {
           // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
-#if FHE_BFLY == 2
           x[j] = csubk(csubk(shoup_q3(sum, nf0.x, nf0.y, nq), q2), q);
           x[jj] = csubk(csubk(shoup_q3(dif, nf1.x, nf1.y, nq), q2), q);
-#else
-          x[j] = csub(shoup_lazy(sum, nf0.x, nf0.y, q), q);
-          x[jj] = csub(shoup_lazy(dif, nf1.x, nf1.y, q), q);
-#endif
         } else {
           const ulonglong2 w = twiddle(b, j, bitpos, st);
-#if FHE_BFLY == 2
           x[j] = csubk(sum, q3);
           x[jj] = shoup_q3(dif, w.x, w.y, nq);
-#elif FHE_BFLY == 1
-          x[j] = csub_fast(sum, nq2);
-          x[jj] = shoup_fast(dif, w.x, w.y, nq);
-#else
-          x[j] = csub(sum, q2);
-          x[jj] = shoup_lazy(dif, w.x, w.y, q);
-#endif
         }
       }
     }
@@ -668,35 +544,26 @@ struct LViewC {
   }
 };
 
-// Round-0 global load of one sub-transform into registers (issued ahead of the work that needs
-// it: the kernels below prefetch their next item while computing the current one).
+// Round-0 global load of one sub-transform into registers.
 template <int LOGR, bool FWD, class GIn>
 __device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
   using Rd = Rounds<LOGR>;
   using Lay = Layout<LOGR, FWD ? Rd::kb(0) : Rd::kb_inv(0), FWD ? Rd::lo_fwd(0) : Rd::lo_inv(0)>;
-#if FHE_NTT_ABLATE == 2  // timing-only build: no global loads (synthetic values below q)
-  (void)gin;
-  for (int j = 0; j < kE; ++j) x[j] = ((u64)(Lay::tpos(t) + j) * 0x9e3779b97f4a7c15ull) >> 5;
-#else
   gin.template load<Lay>(x, Lay::tpos(t));
-#endif
 }
 
 // The rest of a 2^LOGR-point pass on values pass_load brought in: rounds exchange through LDS,
 // the last round stores straight to global memory.  Every thread of the LDS-sharing group must
-// call it (it contains the exchange fences; the first one also orders this item's LDS writes
-// after the previous item's LDS reads).
-// `hook` runs once round 0's twiddle loads are in flight (the item loops' prefetch).
+// call it (it contains the exchange fences).
 // H / R0: forward headroom and input range of the pass (fwd_range), in units of q.
 // XOUT: the last round goes out through the LDS in linear order (GView::store_lin) instead of
 // straight from registers, whose last-round positions are E consecutive words per thread, so a
 // direct store instruction writes 16 of every 16 E bytes across 16 E * 64 bytes.
-template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, bool LOOPED, int H, int R0,
-          bool XOUT = false, class GOut, class LV, class Hook = NoHook>
+template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, int H, int R0, bool XOUT = false,
+          class GOut, class LV>
 __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const LV& lv, u32 t,
                                          const ulonglong2* __restrict__ tw, u32 base, u64 q,
-                                         ulonglong2 nf0, ulonglong2 nf1,
-                                         const Hook& hook = Hook{}) {
+                                         ulonglong2 nf0, ulonglong2 nf1) {
   using Rd = Rounds<LOGR>;
   static_for<0, Rd::NR>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
@@ -710,26 +577,13 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
       lds_sync<SYNC>();
       lv.template load<Lay>(x, tp);
     }
-#if FHE_NTT_ABLATE == 1  // timing-only build: no butterflies
-    for (int j = 0; j < kE; ++j) asm volatile("" : "+v"(x[j]));
-#else
     // an opaque twiddle base per round keeps the scheduler from hoisting every round's twiddle
-    // loads to the top (the gathered row passes, item loops: their VGPRs would cost occupancy or
-    // spill); the column pass's few shared twiddles are left to the scheduler
+    // loads to the top (the gathered row passes: their VGPRs would cost occupancy or spill); the
+    // column pass's few shared twiddles are left to the scheduler
     const ulonglong2* twk = tw;
-    if constexpr (LOOPED || GATHER) asm volatile("" : "+s"(twk));
-    if constexpr (k == 0)
-      round_compute<LOGR, KB, LO, FWD, F, GATHER || LOOPED, H, RIN, GATHER>(x, tp, twk, base, q,
-                                                                           nf0, nf1, hook);
-    else
-      round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN>(x, tp, twk, base, q, nf0, nf1);
-#endif
+    if constexpr (GATHER) asm volatile("" : "+s"(twk));
+    round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN>(x, tp, twk, base, q, nf0, nf1);
     if constexpr (k == Rd::NR - 1) {
-#if FHE_NTT_ABLATE == 2
-      u64 acc = 0;
-      for (int j = 0; j < kE; ++j) acc ^= x[j];
-      if (acc == 0x5a5a5a5a5a5a5a5aull) gout.template store<Lay>(x, tp);  // practically never
-#else
       if constexpr (XOUT) {
         constexpr u32 TPS = (1u << LOGR) / kE;
         lds_sync<SYNC>();
@@ -745,12 +599,10 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
       } else {
         gout.template store<Lay>(x, tp);
       }
-#endif
     } else {
-      // round 0's store needs a fence only when the previous item's last LDS reads precede it;
-      // the (free) wave-local fence also keeps the row passes' LDS stores together after the
-      // butterflies, which measured faster than letting them interleave
-      if (k > 0 || LOOPED || SYNC == kWaveSync) lds_sync<SYNC>();
+      // the (free) wave-local fence before round 0's store keeps the row passes' LDS stores
+      // together after the butterflies, which measured faster than letting them interleave
+      if (k > 0 || SYNC == kWaveSync) lds_sync<SYNC>();
       lv.template store<Lay>(x, tp);
     }
   });
@@ -777,77 +629,49 @@ struct Geo {
   static_assert(N1 >= kElog - 1 && N2 >= kElog, "log N too small for this kernel family");
 };
 
-// Item loops.  A pass kernel runs a one-generation grid (tools: launch_items) and each
-// workgroup walks items b, b + grid, b + 2 grid, ...; the next item's round-0 loads are issued
-// before the current item's butterflies, so HBM latency hides behind compute instead of
-// needing more resident waves (LDS caps these kernels at 4 workgroups per CU).  grid is a
-// multiple of 8, so an item keeps the XCD (blockIdx % 8) its index maps to.
-
-// Column pass over items (p, l, tile) of src/dst [polys][nlimbs][N] via PolyMap.
+// Column pass, one workgroup per item (p, l, tile) of src/dst [polys][nlimbs][N] via PolyMap.
 // NTL / NTS: non-temporal loads of the source / stores of the destination (see GView).
+// (Persistent grids looping over items with a register prefetch of the next one measured slower:
+// vmcnt retires in issue order, so every twiddle wait also waited for the prefetch, and the
+// prefetch registers pushed the column kernel into spills -- DESIGN.md §8.)
 template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false>
-__global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
-    FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_ntt_col(const u64* __restrict__ src,
-                                                      const u64* __restrict__ src2,
-                                                      u64* __restrict__ dst, u32 nlimbs,
-                                                      u32 limb0, PolyMap pm, u32 items,
-                                                      const ulonglong2* __restrict__ tw_all,
-                                                      const ulonglong2* __restrict__ nfold,
-                                                      const ModParams* __restrict__ mods) {
+__global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_ntt_col(
+    const u64* __restrict__ src, const u64* __restrict__ src2, u64* __restrict__ dst, u32 nlimbs,
+    u32 limb0, PolyMap pm, u32 items, const ulonglong2* __restrict__ tw_all,
+    const ulonglong2* __restrict__ nfold, const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[G::LDS_C];
   const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
   const LViewC<G::SUBS_C> lv{lds + sub};
-  struct Item {  // all wave-uniform
-    u32 limb;
-    const u64* s;
-    u64* d;
-  };
-  auto decode = [&](u32 it) {
-    const u32 tile = it % G::TILES_C, pl = it / G::TILES_C;
-    const u32 l = pl % nlimbs, p = pl / nlimbs;
-    const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
-    const u64* s = pm.second(p) ? src2 + pm.src2(p) : src + pm.src(p);
-    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), s + loc, dst + pm.dst(p) + loc};
-  };
-  u32 it = blockIdx.x;
+  const u32 it = blockIdx.x;
   if (it >= items) return;
-  Item cur = decode(it);
-  u64 x[kE], y[kE];
-  pass_load<G::N1, FWD>(GView<G::R2, NTL>{const_cast<u64*>(cur.s), sub}, t, x);
-  while (true) {
-    const u32 nx = it + gridDim.x;
-    const bool more = kLoopCol && FWD && nx < items;
-    const Item nxt = more ? decode(nx) : cur;
-    auto prefetch = [&] {
-      if (more) pass_load<G::N1, FWD>(GView<G::R2>{const_cast<u64*>(nxt.s), sub}, t, y);
-    };
-    ulonglong2 nf0 = {0, 0}, nf1 = {0, 0};
-    if (!FWD) {
-      nf0 = nfold[4 * cur.limb];
-      nf1 = nfold[4 * cur.limb + 1];
-    }
-    using GOut = GView<G::R2, false, NTS>;
-    pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, kLoopCol && FWD, H, 1>(
-        x, GOut{cur.d, sub}, lv, t, tw_all + (u64)cur.limb * N, 1u, mods[cur.limb].q,
-        nf0, nf1, prefetch);
-    if (!more) break;
-    it = nx;
-    cur = nxt;
-#pragma unroll
-    for (int j = 0; j < kE; ++j) x[j] = y[j];
+  const u32 tile = it % G::TILES_C, pl = it / G::TILES_C;
+  const u32 l = pl % nlimbs, p = pl / nlimbs;
+  const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
+  const u64* s = (pm.second(p) ? src2 + pm.src2(p) : src + pm.src(p)) + loc;
+  const u32 limb = __builtin_amdgcn_readfirstlane(limb0 + l);
+  u64 x[kE];
+  pass_load<G::N1, FWD>(GView<G::R2, NTL>{const_cast<u64*>(s), sub}, t, x);
+  ulonglong2 nf0 = {0, 0}, nf1 = {0, 0};
+  if (!FWD) {
+    nf0 = nfold[4 * limb];
+    nf1 = nfold[4 * limb + 1];
   }
+  pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, H, 1>(
+      x, GView<G::R2, false, NTS>{dst + pm.dst(p) + loc, sub}, lv, t, tw_all + (u64)limb * N, 1u,
+      mods[limb].q, nf0, nf1);
 }
 
-// Row pass over items (l, p, tile): the limb follows the XCD and the poly varies fastest, so the
-// workgroups of one XCD reuse a row's twiddles while they are hot.
+// Row pass, one workgroup per item (l, p, tile): the limb follows the XCD and the poly varies
+// fastest, so the workgroups of one XCD reuse a row's twiddles while they are hot.  The forward
+// stores its last round in linear order through the LDS (XOUT); the inverse loads its first round
+// that way.
 template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false>
-__global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
-                                                      u64* __restrict__ dst, u32 nlimbs,
-                                                      u32 limb0, PolyMap pm, u32 items,
-                                                      const ulonglong2* __restrict__ tw_all,
-                                                      const ModParams* __restrict__ mods) {
+__global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src, u64* __restrict__ dst, u32 nlimbs,
+                                    u32 limb0, PolyMap pm, u32 items,
+                                    const ulonglong2* __restrict__ tw_all,
+                                    const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[G::LDS_R];
@@ -855,62 +679,37 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src,
   const u32 t = threadIdx.x % G::TPS_R, sub = threadIdx.x / G::TPS_R;
   const LView<1, true> lv{lds + sub * G::RS};
   const u32 polys = items / (nlimbs * G::TILES_R);
-  struct Item {  // all wave-uniform; this lane's row is row0 + sub
-    u32 limb, row0;
-    u64 src, dst;
-  };
-  auto decode = [&](u32 it) {
-    u32 l, rest;
-    xcd_limb_split(it, nlimbs, items / nlimbs, l, rest);
-    const u32 p = rest % polys, tile = rest / polys;
-    const u32 row0 = tile * G::SUBS_R;
-    const u64 loc = (u64)l * N + (u64)row0 * G::R2;
-    return Item{(u32)__builtin_amdgcn_readfirstlane(limb0 + l), row0, pm.src(p) + loc, pm.dst(p) + loc};
-  };
-  const u32 lane = sub * G::R2;
-  u32 it = blockIdx.x;
+  const u32 it = blockIdx.x;
   if (it >= items) return;
-  Item cur = decode(it);
-  u64 x[kE], y[kE];
-  if constexpr (!FWD && kRowXin && !kLoopRow) {
+  u32 l, rest;
+  xcd_limb_split(it, nlimbs, items / nlimbs, l, rest);
+  const u32 p = rest % polys, tile = rest / polys;
+  const u32 row0 = tile * G::SUBS_R;
+  const u64 loc = (u64)l * N + (u64)row0 * G::R2;
+  const u32 limb = __builtin_amdgcn_readfirstlane(limb0 + l);
+  const u32 lane = sub * G::R2;
+  const GView<1, NTL> gin{const_cast<u64*>(src) + pm.src(p) + loc, lane};
+  u64 x[kE];
+  if constexpr (!FWD) {
     // the inverse's round 0 owns E consecutive words per thread: load the row linearly and
     // redistribute through the LDS (the mirror of pass_run's XOUT store)
     using Rd = Rounds<G::N2>;
     using Lay0 = Layout<G::N2, Rd::kb_inv(0), Rd::lo_inv(0)>;
-    GView<1, NTL>{const_cast<u64*>(src) + cur.src, lane}.template load_lin<G::TPS_R>(x, t);
+    gin.template load_lin<G::TPS_R>(x, t);
 #pragma unroll
     for (int jj = 0; jj < kE / 2; ++jj) {
-      const u32 p = 2 * t + 2 * G::TPS_R * jj;
-      lv.s[lv.idx(p)] = x[2 * jj];
-      lv.s[lv.idx(p + 1)] = x[2 * jj + 1];
+      const u32 q = 2 * t + 2 * G::TPS_R * jj;
+      lv.s[lv.idx(q)] = x[2 * jj];
+      lv.s[lv.idx(q + 1)] = x[2 * jj + 1];
     }
     lds_sync<kWaveSync>();
     lv.template load<Lay0>(x, Lay0::tpos(t));
   } else {
-    pass_load<G::N2, FWD>(GView<1, NTL>{const_cast<u64*>(src) + cur.src, lane}, t, x);
+    pass_load<G::N2, FWD>(gin, t, x);
   }
-  while (true) {
-    const u32 nx = it + gridDim.x;
-    const bool more = kLoopRow && nx < items;
-    const Item nxt = more ? decode(nx) : cur;
-    auto prefetch = [&] {
-      if (more) pass_load<G::N2, FWD>(GView<1>{const_cast<u64*>(src) + nxt.src, lane}, t, y);
-    };
-    pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, kLoopRow, H,
-             fwd_range(1, G::N1, H), FWD && kRowXout>(
-        x, GView<1, false, NTS>{dst + cur.dst, lane}, lv, t, tw_all + (u64)cur.limb * N,
-#if FHE_NTT_ABLATE == 3  // timing-only build: every row uses row 0's twiddles (cache-resident)
-        (u32)G::R1,
-#else
-        (u32)G::R1 + cur.row0 + sub,
-#endif
-        mods[cur.limb].q, {0, 0}, {0, 0}, prefetch);
-    if (!more) break;
-    it = nx;
-    cur = nxt;
-#pragma unroll
-    for (int j = 0; j < kE; ++j) x[j] = y[j];
-  }
+  pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, H, fwd_range(1, G::N1, H),
+           FWD>(x, GView<1, false, NTS>{dst + pm.dst(p) + loc, lane}, lv, t,
+                tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, mods[limb].q, {0, 0}, {0, 0});
 }
 
 // Fused HomMult row kernel: rows of the 4 column-transformed inputs (layout [batch][4][nlimbs][N]
@@ -928,40 +727,24 @@ struct HmGeo {
   static constexpr int ROWW = 4 * G::RS;                     // LDS words per row (4 slots)
   static constexpr int TILES = G::R1 / ROWS;
   static_assert(64 % LANES_ROW == 0 || LANES_ROW % 64 == 0, "row group vs wavefront");
-  // FHE_HM_POLY_MAJOR: thread group g = one polynomial spread over whole wavefronts, so during the
+  // Thread group g = one polynomial spread over whole wavefronts ("poly-major"), so during the
   // 3-poly inverse the 4th group is a whole idle wave (its SIMD slots go to other waves) instead
   // of idle lanes inside every wave (measured: VALUBusy ~100 % with 77 % lane utilisation).
   // A polynomial's rows then sit in one wavefront, so its round exchanges stay wave-local and
   // only the tensor (reading all four slots) needs the block barrier.
-  static constexpr bool POLY_MAJOR = FHE_HM_POLY_MAJOR != 0;
-  static constexpr int SYNC_TENSOR = (!POLY_MAJOR && LANES_ROW <= 64) ? kWaveSync : kBlockSync;
-  static constexpr int SYNC_ROUND = (POLY_MAJOR || LANES_ROW <= 64) ? kWaveSync : kBlockSync;
+  static constexpr int SYNC_TENSOR = kBlockSync;
+  static constexpr int SYNC_ROUND = kWaveSync;
 };
 
-// FHE_HM_NT: non-temporal workspace reads / output writes in the fused kernel and the column inverse.
-#ifndef FHE_HM_NT
-#define FHE_HM_NT 1
-#endif
-constexpr bool kHmNT = FHE_HM_NT != 0;
-// FHE_HM_COLF_NTL: the column-forward pass reads a and b non-temporally (read once; +0.7 %).
-#ifndef FHE_HM_COLF_NTL
-#define FHE_HM_COLF_NTL 1
-#endif
-// FHE_KS_NT: the key-switch's extended rows (written by k_modup_col, read once by k_ks_row_inner)
-// go through non-temporal stores and loads (fused row kernel 403 -> 379 us per step, +1.5 %).
-#ifndef FHE_KS_NT
-#define FHE_KS_NT 1
-#endif
-constexpr bool kKsNT = FHE_KS_NT != 0;
-// FHE_NTT_NT_IN / FHE_NTT_NT_OUT: standalone NTT -- first pass's loads / second pass's stores
-// non-temporal.  Measured slower (-8 % / -5 % NTT/s with the bench's back-to-back transforms of
-// one 256 MiB batch, which the Infinity Cache partly holds); off, kept as A/B switches.
-#ifndef FHE_NTT_NT_IN
-#define FHE_NTT_NT_IN 0
-#endif
-#ifndef FHE_NTT_NT_OUT
-#define FHE_NTT_NT_OUT 0
-#endif
+// Cache policy (measured per access): non-temporal workspace reads / output writes
+// in the fused HomMult kernel and its column inverse (-2 % / -6 %), non-temporal a, b reads in the
+// HomMult column forward (read once, +0.7 % HomMult/s), non-temporal stores / loads of the
+// key-switch's extended rows (written by k_modup_col, read once by k_ks_row_inner: fused row
+// kernel -6 %).  The standalone NTT stays cached: its second pass re-reads what the first wrote,
+// and the Infinity Cache serves part of it (non-temporal there: -5 ... -8 % NTT/s).
+constexpr bool kHmNT = true;
+constexpr bool kKsNT = true;
+
 template <int LOGN, int HR = 8>
 __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
                                                           u64* __restrict__ d, u32 nlimbs,
@@ -983,18 +766,11 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   const ModParams m = mods[limb];
   const u64 q = m.q;
   const u64 limbN = (u64)nlimbs * N;
-  u32 sub, grp, t;
-  if constexpr (H::POLY_MAJOR) {  // [poly][row][lane]
-    // rotate which wave gets which poly per workgroup: the wave that idles through the 3-poly
-    // inverse must not land on the same SIMD in every workgroup
-    grp = (threadIdx.x / (H::ROWS * H::TPS) + blockIdx.x) % 4;
-    sub = (threadIdx.x / H::TPS) % H::ROWS;
-    t = threadIdx.x % H::TPS;
-  } else {  // [row][poly][lane]
-    sub = threadIdx.x / H::LANES_ROW;
-    grp = (threadIdx.x % H::LANES_ROW) / H::TPS;
-    t = threadIdx.x % H::TPS;
-  }
+  // [poly][row][lane]; which wave gets which poly rotates per workgroup: the wave that idles
+  // through the 3-poly inverse must not land on the same SIMD in every workgroup
+  u32 grp = (threadIdx.x / (H::ROWS * H::TPS) + blockIdx.x) % 4;
+  const u32 sub = (threadIdx.x / H::TPS) % H::ROWS;
+  const u32 t = threadIdx.x % H::TPS;
   const u32 row = tile * H::ROWS + sub;
   const u64 loc = (u64)l * N + (u64)row * G::R2;
   const ulonglong2* tf = twf + (u64)limb * N;
@@ -1038,7 +814,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   // rows take (inputs below 3q); R is folded back in with N^-1 by the column inverse.  d1's sum of
   // two products stays below 8q^2 < q R (q < 2^61).
   // Poly-major groups are whole wavefronts, so the group switch is a uniform branch per wave.
-  if constexpr (H::POLY_MAJOR) grp = __builtin_amdgcn_readfirstlane(grp);
+  grp = __builtin_amdgcn_readfirstlane(grp);
   const bool active = grp < 3;
   const u32 aoff = grp == 2 ? G::RS : 0, boff = grp == 2 ? 3 * G::RS : 2 * G::RS;
   // subtractive REDC (mont_redc): no carry-in term, 3 VALU fewer per element than the additive one
@@ -1101,7 +877,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
 // skipped) -> limb r < n0 ? base0 + r : base1 + (r - n0).
 template <int LOGN, int H, int S>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
-    FHE_NTT_MIN_WAVES, FHE_NTT_MAX_WAVES))) void k_modup_col(const u64* __restrict__ y,
+    4, 8))) void k_modup_col(const u64* __restrict__ y,
                                                         u64* __restrict__ ext, u64 rn, u32 T,
                                                         u32 skip_at, u32 skip_len, u32 n0,
                                                         u32 base0, u32 base1, u32 batch,
@@ -1145,7 +921,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     for (int k = 0; k < S; ++k) acc.add(split30(yb[(u64)k * N + i]), h2[k]);
     x[j] = acc.mont(m.q, m.qinv);
   }
-  pass_run<G::N1, true, kNotFinal, kBlockSync, false, false, H, 1>(
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 1>(
       x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
       tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
 }
@@ -1219,7 +995,7 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   const FinishView fo{(h ? ks1 : ks0) + ((u64)b * nq + l) * N + rloc,
                       acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc, lane, q,
                       pinv[limb]};
-  pass_run<G::N2, true, kFinalFwd, kWaveSync, true, false, H, fwd_range(1, G::N1, H), kRowXout>(
+  pass_run<G::N2, true, kFinalFwd, kWaveSync, true, H, fwd_range(1, G::N1, H), true>(
       x, fo, lv, t, tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, q, {0, 0}, {0, 0});
 }
 
@@ -1360,30 +1136,9 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
   }
 }
 
-// One-generation grid for an item-loop kernel: as many workgroups as fit on the device at once
-// (occupancy queried once per kernel), never more than the items, rounded up to a multiple of 8
-// so item -> XCD placement holds (surplus workgroups exit at once).
-#ifndef FHE_ITEM_WG_PER_CU
-#define FHE_ITEM_WG_PER_CU 0  // 0: ask the occupancy API; > 0: A/B override
-#endif
-#ifndef FHE_ITEM_GENERATIONS
-#define FHE_ITEM_GENERATIONS 1
-#endif
-template <auto K, bool LOOP>
-dim3 item_grid(const fhe_ctx* c, int threads, u64 items) {
-  if (!LOOP) return dim3((u32)((items + 7) / 8 * 8));  // one workgroup per item
-  static const int per_cu = [threads] {
-    int nb = FHE_ITEM_WG_PER_CU;
-    if (nb == 0 &&
-        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, K, threads, 0) != hipSuccess || nb < 1))
-      nb = 1;
-    if (getenv("FHE_DEBUG_GRID")) fprintf(stderr, "item_grid: %d workgroups per CU\n", nb);
-    return nb * FHE_ITEM_GENERATIONS;
-  }();
-  u64 g = std::min<u64>(items, (u64)per_cu * (c->num_cus > 0 ? c->num_cus : 256));
-  g = (g + 7) / 8 * 8;
-  return dim3((u32)g);
-}
+// One workgroup per item, rounded up to a multiple of 8 so item -> XCD placement holds (surplus
+// workgroups exit at once).
+inline dim3 item_grid(u64 items) { return dim3((u32)((items + 7) / 8 * 8)); }
 
 // The inverse passes' H: the lazy inverse does not depend on the forward headroom (one build for
 // H = 8 and 16); wide contexts (H = 2) take the exact one.
@@ -1396,16 +1151,15 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
   using G = Geo<LOGN>;
   const u64 ir = (u64)polys * nlimbs * G::TILES_R;
   const PolyMap pm{1, sp, 0, dp, 0, 0};
-  constexpr bool IN = FHE_NTT_NT_IN != 0, OUT = FHE_NTT_NT_OUT != 0;
   const ulonglong2* twf = c->d_tw_fwd;
   const ulonglong2* twi = c->d_tw_inv;
   if (fwd)  // the forward's second pass
-    k_ntt_row<LOGN, true, HD, false, OUT>
-        <<<item_grid<k_ntt_row<LOGN, true, HD, false, OUT>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
+    k_ntt_row<LOGN, true, HD>
+        <<<item_grid(ir), G::THR_R,
            0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, twf, c->d_mods);
   else  // the inverse's first pass
-    k_ntt_row<LOGN, false, inv_h(HD), IN, false>
-        <<<item_grid<k_ntt_row<LOGN, false, inv_h(HD), IN, false>, kLoopRow>(c, G::THR_R, ir), G::THR_R,
+    k_ntt_row<LOGN, false, inv_h(HD)>
+        <<<item_grid(ir), G::THR_R,
            0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, twi, c->d_mods);
 }
 
@@ -1420,10 +1174,9 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   // the second pass runs in place on dst
   const PolyMap pd = flat_map(dpstride);
   const u64 ic = pl * G::TILES_C;
-  constexpr bool IN = FHE_NTT_NT_IN != 0, OUT = FHE_NTT_NT_OUT != 0;
   if (fwd) {
-    k_ntt_col<LOGN, true, HD, IN, false>
-        <<<item_grid<k_ntt_col<LOGN, true, HD, IN, false>, kLoopCol>(c, G::THR_C, ic),
+    k_ntt_col<LOGN, true, HD>
+        <<<item_grid(ic),
            G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd,
                              c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_fwd");
@@ -1432,8 +1185,8 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   } else {
     row_pass<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_inv");
-    k_ntt_col<LOGN, false, inv_h(HD), false, OUT>
-        <<<item_grid<k_ntt_col<LOGN, false, inv_h(HD), false, OUT>, false>(c, G::THR_C, ic),
+    k_ntt_col<LOGN, false, inv_h(HD)>
+        <<<item_grid(ic),
            G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv,
                              nfold ? nfold : c->d_nfold, c->d_mods);
     prof_mark(s, "ntt_col_inv");
@@ -1453,8 +1206,8 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   // over the 4 polys of every ciphertext pair (group of 4: slots 0, 1 from a, slots 2, 3 from b)
   const PolyMap to_x{4, 2 * limbN, limbN, 4 * limbN, limbN, 2};
   const u64 ic = (u64)batch * 4 * nlimbs * G::TILES_C;
-  constexpr bool FL = FHE_HM_COLF_NTL != 0;
-  k_ntt_col<LOGN, true, HD, FL><<<item_grid<k_ntt_col<LOGN, true, HD, FL>, kLoopCol>(c, G::THR_C, ic),
+  constexpr bool FL = true;  // a, b are read once: non-temporal
+  k_ntt_col<LOGN, true, HD, FL><<<item_grid(ic),
                                   G::THR_C, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic,
                                                     c->d_tw_fwd, c->d_nfold, c->d_mods);
   prof_mark(s, "hm_col_fwd");
@@ -1465,7 +1218,7 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
   k_ntt_col<LOGN, false, inv_h(HD), kHmNT, kHmNT>
-      <<<item_grid<k_ntt_col<LOGN, false, inv_h(HD), kHmNT, kHmNT>, false>(c, G::THR_C, ii),
+      <<<item_grid(ii),
          G::THR_C, 0, s>>>(d, nullptr, d, nlimbs, limb0, flat_map(limbN), (u32)ii, c->d_tw_inv,
                            c->d_nfold + 2, c->d_mods);
   prof_mark(s, "hm_col_inv");
@@ -1493,7 +1246,7 @@ void col_fwd_pass(const fhe_ctx* c, const u64* src, u64 sp, u64* dst, u64 dp, u3
   using G = Geo<LOGN>;
   const u64 ic = (u64)polys * nlimbs * G::TILES_C;
   const PolyMap pm{1, sp, 0, dp, 0, 0};
-  k_ntt_col<LOGN, true, HD><<<item_grid<k_ntt_col<LOGN, true, HD>, kLoopCol>(c, G::THR_C, ic),
+  k_ntt_col<LOGN, true, HD><<<item_grid(ic),
                               G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic,
                                                 c->d_tw_fwd, c->d_nfold, c->d_mods);
 }
@@ -1667,37 +1420,12 @@ static int hommult_chunk(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u
   return kUnsupported;
 }
 
-// FHE_HM_SPLIT: HomMult batches of at least two ciphertexts run as two half-batch pipelines on
-// the caller's stream and a context-owned helper stream (event fork / join, graph-capturable),
-// so one half's memory-heavy column passes share the CUs with the other half's VALU-bound fused
-// row kernel instead of alternating with it.
-#ifndef FHE_HM_SPLIT
-#define FHE_HM_SPLIT 0  // measured: no gain (37.2k vs 36.9k HomMult/s); kept as an A/B switch
-#endif
-
+// (Two half-batch pipelines on two streams, so one half's memory-bound column passes share the CUs
+// with the other half's VALU-bound fused row kernel, measured no gain: 37.2k vs 36.9k HomMult/s.)
 int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                    u32 nlimbs, void* ws, hipStream_t s) {
   if ((u64)batch * nlimbs == 0) return kOk;
-  u64* x = static_cast<u64*>(ws);
-  if (!FHE_HM_SPLIT || batch < 2) return hommult_chunk(c, d, a, b, batch, limb0, nlimbs, x, s);
-  auto* cc = const_cast<fhe_ctx*>(c);
-  std::lock_guard<std::mutex> lock(cc->aux_mutex);
-  if (!cc->aux_stream) {
-    FHE_HIP_CHECK(hipStreamCreateWithFlags(&cc->aux_stream, hipStreamNonBlocking));
-    FHE_HIP_CHECK(hipEventCreateWithFlags(&cc->aux_fork, hipEventDisableTiming));
-    FHE_HIP_CHECK(hipEventCreateWithFlags(&cc->aux_join, hipEventDisableTiming));
-  }
-  const u32 h1 = batch / 2, h2 = batch - h1;
-  const u64 pn = (u64)nlimbs * c->n;  // one polynomial of this limb window
-  FHE_HIP_CHECK(hipEventRecord(cc->aux_fork, s));
-  FHE_HIP_CHECK(hipStreamWaitEvent(cc->aux_stream, cc->aux_fork, 0));
-  int rc = hommult_chunk(c, d + (u64)h1 * 3 * pn, a + (u64)h1 * 2 * pn, b + (u64)h1 * 2 * pn, h2,
-                         limb0, nlimbs, x + (u64)h1 * 4 * pn, cc->aux_stream);
-  if (rc) return rc;
-  FHE_HIP_CHECK(hipEventRecord(cc->aux_join, cc->aux_stream));
-  if ((rc = hommult_chunk(c, d, a, b, h1, limb0, nlimbs, x, s))) return rc;
-  FHE_HIP_CHECK(hipStreamWaitEvent(s, cc->aux_join, 0));
-  return kOk;
+  return hommult_chunk(c, d, a, b, batch, limb0, nlimbs, static_cast<u64*>(ws), s);
 }
 
 #endif  // FHE_NTT_KS_ONLY

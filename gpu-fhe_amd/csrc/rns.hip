@@ -30,15 +30,6 @@ inline KOff rows_contiguous(u32 S, u64 n) {
   for (u32 i = 0; i < S; ++i) k.o[i] = (u64)i * n;
   return k;
 }
-#ifndef FHE_KS_FUSED
-#define FHE_KS_FUSED 1
-#endif
-#ifndef FHE_MODUP_FUSED
-#define FHE_MODUP_FUSED 1
-#endif
-#ifndef FHE_MODDOWN_FUSED
-#define FHE_MODDOWN_FUSED 1
-#endif
 
 // out row r -> ctx limb: r < n0 ? base0 + r : base1 + (r - n0)
 struct RowMap {
@@ -374,16 +365,16 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   const u64 acc_ws = B * rn;
   const RowMap map{nlimbs, limb0, L};
   int rc;
-  // FHE_KS_FUSED: for dnum <= 4 the digits get only their column-forward pass here, and one fused
+  // Fused path: for dnum <= 4 the digits get only their column-forward pass here, and one fused
   // kernel (ntt.hip, k_ks_row_inner) runs every digit's row-forward pass and the inner product
   // (no NTT-form ext in HBM, no separate inner-product pass); otherwise full NTTs + k_ks_inner.
   // Wide contexts (a modulus >= 2^61) take the unfused kernels: the fused ones rely on lazy
   // ranges and 128-bit sums that need q < 2^61.
-  const bool fused = FHE_KS_FUSED && c->dnum <= 4 && !c->wide;
-  // FHE_MODUP_FUSED (with the fused row kernel, digits of <= 4 limbs): the base conversion runs
+  const bool fused = c->dnum <= 4 && !c->wide;
+  // Fused ModUp (with the fused row kernel, digits of <= 4 limbs): the base conversion runs
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
   // digit's source rows; the extended rows are never written in coefficient form.
-  const bool fused_up = fused && FHE_MODUP_FUSED && alpha <= 4;
+  const bool fused_up = fused && alpha <= 4;
   u64* yws = conv + 2 * B * (u64)nlimbs * n;  // [B][alpha][N]
   auto ntt_fwd = [&](u64* p, u32 l0, u32 nl) {
     return fused ? launch_ntt_col_fwd(c, p, rn, p, rn, batch, l0, nl, s)
@@ -441,8 +432,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   prof_mark(s, "ks_inner");
   // ModDown: INTT the P rows of both accumulators, convert P -> own Q-limbs, NTT, finish
   u64* accp = acc + (u64)nlimbs * n;
-  const bool fused_down = fused && FHE_MODDOWN_FUSED && K <= 4 && (u64)c->dnum * rows >= 2 * (u64)K;
-  // FHE_MODDOWN_FUSED (fused path, K <= 4): the P -> Q conversion runs inside the column-forward
+  const bool fused_down = fused && K <= 4 && (u64)c->dnum * rows >= 2 * (u64)K;
+  // Fused ModDown (fused path, K <= 4): the P -> Q conversion runs inside the column-forward
   // pass of the conversion NTT (k_modup_col, as ModUp), on the P rows the INTT has already scaled
   // into the ext region (free once the inner product has run): conv is never written in
   // coefficient form.

@@ -1,5 +1,5 @@
 """CPU models of the word-level reductions in gpu-fhe_amd/csrc/modarith.hpp, checked against
-exact big-integer arithmetic: the range claims the lazy NTT butterflies rely on (FHE_BFLY = 2 in
+exact big-integer arithmetic: the range claims the lazy NTT butterflies rely on (round_compute in
 csrc/ntt.hip) and the Montgomery tensor of the fused HomMult kernel.  Each model follows the
 device code's 32-bit partial products step by step (same truncations, same carries)."""
 import random
@@ -75,7 +75,7 @@ def test_mont_reduce_lazy(q):
 
 @pytest.mark.parametrize("q", _moduli())
 def test_lazy_butterfly_ranges(q):
-    """Forward CT values stay in [0, 8q) and inverse GS values in [0, 3q) (FHE_BFLY = 2)."""
+    """Forward CT values stay in [0, 8q) and inverse GS values in [0, 3q) (round_compute, H = 8)."""
     rng = random.Random(q + 2)
     for _ in range(2000):
         w = rng.randrange(q)

@@ -1,7 +1,7 @@
 // Integer-ALU ceiling for the NTT butterflies (measurement infrastructure for bench.py's
 // `roofline_alu`; not part of libfhecore).
 //
-// Runs the exact butterfly instruction sequences of csrc/ntt.hip round_compute (FHE_BFLY = 2,
+// Runs the exact butterfly instruction sequences of csrc/ntt.hip round_compute (the lazy forms,
 // lazy, headroom H = 16) on register-resident data at full occupancy, with no memory traffic:
 //   forward  Cooley-Tukey, folded X-operand (shoup_q3_add), the 8q reduction every other stage
 //            (the row passes' schedule), outputs s and (2u + 3q) - s;
