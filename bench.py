@@ -47,7 +47,8 @@ def parse():
     # ramp (W=5, K=20 reads ~15 % low at N=2^16, L=8); the defaults time the sustained rate
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch", "mulrelin", "ntt-batch"],
+    ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch", "mulrelin", "ntt-batch",
+                                           "vec"],
                     default="hommult")
     ap.add_argument("--batch", type=int, default=None,
                     help="ciphertexts per GPU per step (default 64 for hommult -- the throughput "
@@ -303,6 +304,48 @@ def run_hommult(args, world, rank):
     return out, cpu
 
 
+def run_vec(args, world, rank):
+    """The reference's own operators (vec_add / vec_sub / vec_mul, /root/reference/arithmetic.py:3-13,
+    = poly_mul_pointwise in the NTT domain) through the context kernel k_vec_ctx: one step = one
+    add, one sub and one mul over `batch` polynomials x 8 limbs x N = 2^16 on this rank's limbs.
+    HBM-bound: 24 B per coefficient per op (two reads, one write)."""
+    L = 8
+    shard = fdist.LimbShard(L, world, rank)
+    n = 1 << args.log_n
+    ctx = fc.Context(args.log_n, L=L)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(5 + rank)
+    mods = ctx.moduli[shard.lo:shard.hi]
+    polys = 2 * args.batch
+    a = uniform_limbs(gen, mods, (polys,), n)
+    b = uniform_limbs(gen, mods, (polys,), n)
+    out = torch.empty_like(a)
+    lib = load()
+
+    def step():
+        for fn in (lib.fhe_vec_add, lib.fhe_vec_sub, lib.fhe_vec_mul):
+            check(fn(ctx.handle, out.data_ptr(), a.data_ptr(), b.data_ptr(), polys, shard.lo,
+                     shard.nlimbs, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                  "fhe_vec")
+
+    dt, kavg = timed(step, args, world, 8 * args.steps + 8)
+    coeffs = polys * shard.nlimbs * n
+    per_op = coeffs * 24
+    ops_per_s = 3 * coeffs * world * args.steps / dt
+    out_line = {"metric": "vec_add/vec_sub/vec_mul coefficients/sec at N=2^16, 8 RNS limbs (HBM-bound)",
+                "value": round(ops_per_s, 1), "unit": "coeff-op/s",
+                "ms_per_step": round(dt / args.steps * 1e3, 4),
+                "config": {"workload": "reference vec_add + vec_sub + vec_mul (k_vec_ctx)",
+                           "log_n": args.log_n, "limbs": L, "polys_per_gpu": polys,
+                           "parallelism": f"rns-limb-shard x{world}"},
+                "kernel_ms": {k: round(v, 4) for k, v in kavg.items()}}
+    for k, v in kavg.items():
+        out_line["roofline_" + k] = roofline(k, per_op, v, {"log_n": args.log_n, "polys": polys})
+    dom = max(kavg, key=kavg.get)
+    out_line["roofline"] = roofline(dom, per_op, kavg[dom], {"log_n": args.log_n, "polys": polys})
+    return out_line, None
+
+
 def run_ntt(args, world, rank):
     L = 8
     shard = fdist.LimbShard(L, world, rank)
@@ -530,7 +573,7 @@ def main():
     if args.batch is None:
         args.batch = 64 if args.workload == "hommult" else 16
     world, rank = dist_setup(args)
-    run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch,
+    run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch, "vec": run_vec,
            "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch}[args.workload]
     out, cpu = run(args, world, rank)
     if rank == 0:

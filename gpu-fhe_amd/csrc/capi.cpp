@@ -258,9 +258,14 @@ int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t
   // c_all = INTT(d2) lives at the tail of the workspace (out of place: no copy of d2)
   const size_t call = (size_t)batch * c->L * c->n * sizeof(uint64_t);
   uint64_t* c_all = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + bytes - call);
-  if ((rc = launch_ntt(c, false, d2, c_all, batch, (uint64_t)c->L * c->n, 0, c->L, hs(s))))
+  // a prepared input when the fused ModUp applies: the INTT folds (D^_k)^-1 into its last stage
+  const bool prep = ks_prepared(c);
+  if ((rc = launch_ntt_strided(c, false, d2, (uint64_t)c->L * c->n, c_all, (uint64_t)c->L * c->n,
+                               batch, 0, c->L, hs(s), prep ? c->d_nfold_up : nullptr)))
     return rc;
-  return launch_keyswitch_shard(c, ks0, ks1, c_all, d2, evk_b, evk_a, 0, c->L, batch, ws, hs(s));
+  CAll src = CAll::contiguous(c_all, c->L, c->n);
+  src.scaled = prep;
+  return launch_keyswitch_shard(c, ks0, ks1, src, d2, evk_b, evk_a, 0, c->L, batch, ws, hs(s));
 }
 
 size_t fhe_rescale_workspace(const fhe_ctx* c, uint32_t polys, uint32_t nlimbs) {

@@ -170,6 +170,9 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
   if ((rc = ensure_ws(ctx, fhe_keyswitch_dist_workspace(ctx, comm, batch, chunks), &ws, s)))
     return rc;
   u64* gather = static_cast<u64*>(ws);  // [nc][G][cb][cw][N]
+  // the gathered d2 is the prepared ModUp input when the fused ModUp applies: each rank's INTT
+  // folds (D^_k)^-1 of its limbs' digits into its last stage
+  const bool prep = ks_prepared(ctx);
   void* kws = gather + (u64)nc * G * blk;
   // 1 + 2: every chunk's INTT into its send block, then its gather on the comm stream
   for (u32 k = 0; k < nc; ++k) {
@@ -177,7 +180,8 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
     u64* gbuf = gather + (u64)k * G * blk;
     if (nl && bn &&
         (rc = launch_ntt_strided(ctx, false, d2_own + (u64)b0 * nl * n, (u64)nl * n,
-                                 gbuf + (u64)r * blk, (u64)cw * n, bn, limb0, nl, s)))
+                                 gbuf + (u64)r * blk, (u64)cw * n, bn, limb0, nl, s,
+                                 prep ? ctx->d_nfold_up : nullptr)))
       return rc;
     FHE_HIP_CHECK(hipEventRecord(comm->ev_intt[k], s));
     FHE_HIP_CHECK(hipStreamWaitEvent(comm->stream, comm->ev_intt[k], 0));
@@ -191,7 +195,8 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
     const u32 b0 = k * cb, bn = std::min(batch, b0 + cb) - b0;
     FHE_HIP_CHECK(hipStreamWaitEvent(s, comm->ev_gather[k], 0));
     if (!nl || !bn) continue;
-    const CAll call = CAll::ranked(gather + (u64)k * G * blk, L, G, cb, n);
+    CAll call = CAll::ranked(gather + (u64)k * G * blk, L, G, cb, n);
+    call.scaled = prep;
     const u64 off = (u64)b0 * nl * n;
     if ((rc = launch_keyswitch_shard(ctx, ks0 + off, ks1 + off, call, d2_own + off, evk_b, evk_a,
                                      limb0, nl, bn, kws, s)))

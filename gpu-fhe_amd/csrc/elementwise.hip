@@ -93,6 +93,7 @@ int launch_vec_ctx(const fhe_ctx* c, int op, u64* out, const u64* a, const u64* 
     default: set_error("bad vec op"); return kInvalid;
   }
   FHE_HIP_CHECK(hipGetLastError());
+  prof_mark(s, op == kAdd ? "vec_add" : op == kSub ? "vec_sub" : "vec_mul");
   return kOk;
 }
 

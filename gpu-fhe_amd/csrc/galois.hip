@@ -241,8 +241,13 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
   // key-switch sigma(c1): its coefficient form goes to the tail of the key-switch workspace
   const size_t kbytes = keyswitch_workspace_bytes(c, L, batch);
   u64* c_all = reinterpret_cast<u64*>(reinterpret_cast<char*>(kws) + kbytes) - batch * ln;
-  if ((rc = launch_ntt_strided(c, false, sc1, ln, c_all, ln, batch, 0, L, s))) return rc;
-  if ((rc = launch_keyswitch_shard(c, ks0, ks1, c_all, sc1, rot_b, rot_a, 0, L, batch, kws, s)))
+  const bool prep = ks_prepared(c);  // the INTT emits ModUp's scaled inputs
+  if ((rc = launch_ntt_strided(c, false, sc1, ln, c_all, ln, batch, 0, L, s,
+                               prep ? c->d_nfold_up : nullptr)))
+    return rc;
+  CAll call = CAll::contiguous(c_all, L, n);
+  call.scaled = prep;
+  if ((rc = launch_keyswitch_shard(c, ks0, ks1, call, sc1, rot_b, rot_a, 0, L, batch, kws, s)))
     return rc;
   k_rotate_combine<<<dim3((u32)(n / kThreads), L, batch), kThreads, 0, s>>>(out, ks0, ks1, L,
                                                                            c->log_n, c->d_mods);

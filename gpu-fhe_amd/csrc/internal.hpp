@@ -65,6 +65,9 @@ struct fhe_ctx {
   // fold table for ModDown's INTT of the P rows (entries of limbs L..L+K-1): N^-1 (P^_k)^-1 and
   // psi^-N/2 N^-1 (P^_k)^-1, so the INTT emits the scaled conversion inputs directly
   ulonglong2* d_nfold_down = nullptr;   // [L + K][4]
+  // fold table for the INTT of d2 ahead of a key-switch (entries of limbs 0..L-1): N^-1 (D^_k)^-1
+  // and psi^-N/2 N^-1 (D^_k)^-1 of limb k's digit, so the INTT emits ModUp's scaled inputs
+  ulonglong2* d_nfold_up = nullptr;     // [L + K][4]
 
   void* workspace = nullptr;
   size_t workspace_bytes = 0;
@@ -108,7 +111,9 @@ int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s);
 // y [batch][S][N] into each of its T target rows and runs their column-forward pass, writing the
 // column-passed rows into ext [batch][rows][N] (row stride N, ciphertext stride rn words).
 struct ModUpColArgs {
-  const u64* y;
+  const u64* y;   // source row k of ciphertext b at y + b ybs + yoff[k]
+  u64 ybs;
+  u64 yoff[4];
   u64* ext;
   u64 rn;
   u32 S, T, skip_at, skip_len, n0, base0, base1, batch;
@@ -168,7 +173,15 @@ struct CAll {
     return CAll{p, c, (u64)batch * c * n, (u64)c * n};
   }
   u64 off(u32 l, u64 n) const { return (u64)(l / lpr) * rs + (u64)(l % lpr) * n; }
+  // "prepared" input: every Q-limb k already scaled by (D^_k)^-1 of its digit (the INTT that made
+  // it folded the factor into its last stage, d_nfold_up), so ModUp's scaling pass is skipped
+  bool scaled = false;
 };
+// Whether a key-switch on this context takes the fused ModUp (conversion inside the column pass),
+// which can read a prepared (pre-scaled) input: dnum <= 4, digits of <= 4 limbs, q < 2^61.
+inline bool ks_prepared(const fhe_ctx* c) {
+  return c->K > 0 && c->dnum <= 4 && c->alpha <= 4 && !c->wide;
+}
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
                            u32 nlimbs, u32 batch, void* ws, hipStream_t s);

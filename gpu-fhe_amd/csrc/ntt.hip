@@ -865,9 +865,15 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   });
 }
 
+// The digit's source rows (kernel argument): row k of ciphertext b at y + b ybs + o[k].
+struct ModUpYOff {
+  u64 o[4];
+};
+
 // ModUp column pass (key-switch): the column-forward pass of every extended row of one digit,
 // reading its input straight from the digit's S pre-scaled source rows y_k = [x_k (D^_k)^-1]_{d_k}
-// (coefficient form, rns.hip k_modup_scale) and converting on the fly:
+// (coefficient form: the key-switch's own INTT of d2 folds the factor in (d_nfold_up), else
+// rns.hip k_modup_scale makes them) and converting on the fly:
 //   x = sum_k y_k (D^_k mod t) mod t   (sum < S 2^61 t < t 2^64: Sum30, one Montgomery reduction;
 //                                       hat[k hs + t].y = D^_k 2^64 mod t)
 // so the extended rows are never written in coefficient form (SURVEY §8a' ModUp; the unfused path
@@ -878,6 +884,7 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
 template <int LOGN, int H, int S>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     4, 8))) void k_modup_col(const u64* __restrict__ y,
+                                                        u64 ybs, ModUpYOff yoff,
                                                         u64* __restrict__ ext, u64 rn, u32 T,
                                                         u32 skip_at, u32 skip_len, u32 n0,
                                                         u32 base0, u32 base1, u32 batch,
@@ -911,14 +918,14 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int k = 0; k < S; ++k) h2[k] = split30(hat[(u64)k * hs + limb].y);
   const u32 tp = Lay0::tpos(t);
-  const gptr_u64 yb = (gptr_u64)(y + (u64)b * S * N + (u64)tile * G::SUBS_C + sub);
+  const gptr_u64 yb = (gptr_u64)(y + (u64)b * ybs + (u64)tile * G::SUBS_C + sub);
   u64 x[kE];
 #pragma unroll
   for (int j = 0; j < kE; ++j) {
     const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
     Sum30 acc;
 #pragma unroll
-    for (int k = 0; k < S; ++k) acc.add(split30(yb[(u64)k * N + i]), h2[k]);
+    for (int k = 0; k < S; ++k) acc.add(split30(yb[yoff.o[k] + i]), h2[k]);
     x[j] = acc.mont(m.q, m.qinv);
   }
   pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 1>(
@@ -1296,12 +1303,14 @@ int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst,
 namespace {
 template <int LOGN, int HD>
 int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
+  ModUpYOff yo;
+  for (int k = 0; k < 4; ++k) yo.o[k] = a.yoff[k];
   using G = Geo<LOGN>;
   const dim3 g((u32)((u64)a.T * a.batch * G::TILES_C));
   switch (a.S) {
 #define D(k)                                                                                     \
   case k:                                                                                        \
-    k_modup_col<LOGN, HD, k><<<g, G::THR_C, 0, s>>>(a.y, a.ext, a.rn, a.T, a.skip_at,            \
+    k_modup_col<LOGN, HD, k><<<g, G::THR_C, 0, s>>>(a.y, a.ybs, yo, a.ext, a.rn, a.T, a.skip_at,  \
                                                     a.skip_len, a.n0, a.base0, a.base1, a.batch, \
                                                     a.hat, a.hs, c->d_tw_fwd, c->d_mods);        \
     break;

@@ -96,13 +96,18 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   const size_t kbytes = keyswitch_workspace_bytes(c, L, batch);
   u64* c_all = reinterpret_cast<u64*>(reinterpret_cast<char*>(kws) + kbytes) - batch * ln;
   int rc;
-  if ((rc = launch_ntt_strided(c, false, d + 2 * ln, 3 * ln, c_all, ln, batch, 0, L, s))) return rc;
+  const bool prep = ks_prepared(c);  // the INTT emits ModUp's scaled inputs
+  if ((rc = launch_ntt_strided(c, false, d + 2 * ln, 3 * ln, c_all, ln, batch, 0, L, s,
+                               prep ? c->d_nfold_up : nullptr)))
+    return rc;
   // d2 (NTT form) as a contiguous [batch][L][N] operand: parked in the relinearised-ct buffer,
   // which is free until the combine
   u64* d2 = rl;
   FHE_HIP_CHECK(hipMemcpy2DAsync(d2, ln * sizeof(u64), d + 2 * ln, 3 * ln * sizeof(u64),
                                  ln * sizeof(u64), batch, hipMemcpyDeviceToDevice, s));
-  if ((rc = launch_keyswitch_shard(c, ks0, ks1, c_all, d2, evk_b, evk_a, 0, L, batch, kws, s)))
+  CAll call = CAll::contiguous(c_all, L, n);
+  call.scaled = prep;
+  if ((rc = launch_keyswitch_shard(c, ks0, ks1, call, d2, evk_b, evk_a, 0, L, batch, kws, s)))
     return rc;
   u64* dst = rescale ? rl : out;
   k_relin_combine<<<g, kThreads, 0, s>>>(dst, d, ks0, ks1, L, c->log_n, c->d_mods);

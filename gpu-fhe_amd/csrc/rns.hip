@@ -313,6 +313,16 @@ int build_rns_tables(fhe_ctx* c) {
     for (u32 k = 0; k < K; ++k) pm = mulmod_u64(pm, c->moduli[L + k] % q, q);
     pinv[i] = shoup_pair(powmod_u64(pm, q - 2, q), q);
   }
+  // The INTT of d2 ahead of a key-switch folds ModUp's (D^_k)^-1 into its last stage (N^-1 fold)
+  std::vector<Pair64> nf_up((size_t)4 * M, Pair64{0, 0});
+  for (u32 k = 0; k < L; ++k) {
+    const u64 q = c->moduli[k];
+    const u32 j = k / alpha;
+    const u64 s = mulmod_u64(powmod_u64(c->n % q, q - 2, q), up_inv[(size_t)j * alpha + (k - j * alpha)].x, q);
+    const u64 w = powmod_u64(powmod_u64(c->psi[k], q - 2, q), c->n / 2, q);  // psi^-N/2
+    nf_up[4 * k] = shoup_pair(s, q);
+    nf_up[4 * k + 1] = shoup_pair(mulmod_u64(w, s, q), q);
+  }
   // ModDown's P-row INTT folds the conversion's (P^_k)^-1 into its last stage (N^-1 fold)
   std::vector<Pair64> nf_down((size_t)4 * M, Pair64{0, 0});
   for (u32 k = 0; k < K; ++k) {
@@ -325,7 +335,8 @@ int build_rns_tables(fhe_ctx* c) {
   int rc;
   if ((rc = upload(&c->d_modup_inv, up_inv)) || (rc = upload(&c->d_modup_hat, up_hat)) ||
       (rc = upload(&c->d_moddown_inv, dn_inv)) || (rc = upload(&c->d_moddown_hat, dn_hat)) ||
-      (rc = upload(&c->d_pinv, pinv)) || (rc = upload(&c->d_nfold_down, nf_down)))
+      (rc = upload(&c->d_pinv, pinv)) || (rc = upload(&c->d_nfold_down, nf_down)) ||
+      (rc = upload(&c->d_nfold_up, nf_up)))
     return rc;
   return kOk;
 }
@@ -375,6 +386,10 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
   // digit's source rows; the extended rows are never written in coefficient form.
   const bool fused_up = fused && alpha <= 4;
+  if (call.scaled && !fused_up) {
+    set_error("keyswitch: a prepared (pre-scaled) input needs the fused ModUp (ks_prepared)");
+    return kInvalid;
+  }
   u64* yws = conv + 2 * B * (u64)nlimbs * n;  // [B][alpha][N]
   auto ntt_fwd = [&](u64* p, u32 l0, u32 nl) {
     return fused ? launch_ntt_col_fwd(c, p, rn, p, rn, batch, l0, nl, s)
@@ -388,16 +403,27 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     for (u32 k = 0; k < hi - lo; ++k) ko.o[k] = call.off(lo + k, n);
     if (fused_up) {
       const u32 S = hi - lo;
-      k_modup_scale<<<dim3((u32)(n / kThreads), S, batch), kThreads, 0, s>>>(
-          call.ptr, call.bs, ko, lo, yws, S, c->log_n, c->d_modup_inv + (size_t)j * alpha,
-          c->d_mods);
-      FHE_HIP_CHECK(hipGetLastError());
+      // the conversion's inputs y_k = [x_k (D^_k)^-1]: already in c_all when it is prepared (its
+      // INTT folded the factor in), else one scaling pass into yws
+      const u64* ysrc = call.ptr;
+      u64 ybs = call.bs, yoff[4] = {};
+      for (u32 k = 0; k < S; ++k) yoff[k] = ko.o[k];
+      if (!call.scaled) {
+        k_modup_scale<<<dim3((u32)(n / kThreads), S, batch), kThreads, 0, s>>>(
+            call.ptr, call.bs, ko, lo, yws, S, c->log_n, c->d_modup_inv + (size_t)j * alpha,
+            c->d_mods);
+        FHE_HIP_CHECK(hipGetLastError());
+        ysrc = yws;
+        ybs = (u64)S * n;
+        for (u32 k = 0; k < S; ++k) yoff[k] = (u64)k * n;
+      }
       // this rank's own rows of digit j are skipped: ks_row_inner takes them from d2_own
       const u32 own_lo = std::max(lo, limb0), own_hi = std::min(hi, limb0 + nlimbs);
       const u32 skip_len = own_hi > own_lo ? own_hi - own_lo : 0;
       const u32 skip_at = skip_len ? own_lo - limb0 : rows;
-      const ModUpColArgs ma{yws, e, rn, S, rows - skip_len, skip_at, skip_len, nlimbs, limb0, L,
-                            batch, c->d_modup_hat + (size_t)j * alpha * M, M};
+      const ModUpColArgs ma{ysrc, ybs, {yoff[0], yoff[1], yoff[2], yoff[3]}, e, rn, S,
+                            rows - skip_len, skip_at, skip_len, nlimbs, limb0, L, batch,
+                            c->d_modup_hat + (size_t)j * alpha * M, M};
       if ((rc = launch_modup_col(c, ma, s))) return rc;
       continue;
     }
@@ -445,8 +471,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
                                  c->d_nfold_down)))
       return rc;
     prof_mark(s, "ks_moddown_conv");
-    const ModUpColArgs md{ydn, conv, (u64)nlimbs * n, K, nlimbs, nlimbs, 0, nlimbs, limb0, 0,
-                          2 * batch, c->d_moddown_hat, M};
+    const ModUpColArgs md{ydn, (u64)K * n, {0, n, 2 * n, 3 * n}, conv, (u64)nlimbs * n, K, nlimbs,
+                          nlimbs, 0, nlimbs, limb0, 0, 2 * batch, c->d_moddown_hat, M};
     if ((rc = launch_modup_col(c, md, s))) return rc;
     prof_mark(s, "ks_moddown_col");
     const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch};
