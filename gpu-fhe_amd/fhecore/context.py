@@ -9,6 +9,7 @@ residues, layout [..., limb, N], on a HIP device.
 from __future__ import annotations
 
 import ctypes
+import secrets
 import threading
 from functools import lru_cache
 
@@ -44,6 +45,11 @@ def default_params(log_n: int, L: int, K: int = 0):
 
 
 # ----------------------------------------------------------------------------- device helpers
+
+def _nonce(seed):
+    """The Philox seed of one keygen/encryption call: a fresh CSPRNG draw unless given."""
+    return secrets.randbits(64) if seed is None else int(seed)
+
 
 def _require_device():
     if torch is None or not torch.cuda.is_available():
@@ -329,6 +335,8 @@ class Context:
         return out
 
     # ---- sampling, keys, encryption --------------------------------
+    # seed=None draws a fresh 64-bit nonce from the OS CSPRNG.  An explicit seed is for
+    # reproducible tests: never reuse one per secret key (fhecore.h SECURITY note).
     KIND = {"uniform": 0, "ternary": 1, "error": 2}
 
     def sample(self, kind: str, polys: int, seed: int, tag: int, limb0: int = 0, nlimbs=None):
@@ -340,30 +348,33 @@ class Context:
                                     seed, tag, _stream(out)), "fhe_sample")
         return out
 
-    def keygen_secret(self, seed: int):
+    def keygen_secret(self, seed=None):
         """Ternary secret, NTT form over all L + K limbs: [L + K, N]."""
+        seed = _nonce(seed)
         sk = _empty(self.L + self.K, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_keygen_secret(self._ptr, _ptr(sk), seed, _stream(sk)), "fhe_keygen_secret")
         return sk
 
-    def keygen_public(self, sk, seed: int):
+    def keygen_public(self, sk, seed=None):
+        seed = _nonce(seed)
         pk = _empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_keygen_public(self._ptr, _ptr(pk), _ptr(sk), seed, _stream(pk)),
                   "fhe_keygen_public")
         return pk
 
-    def keygen_switch(self, sk, s_from, seed: int):
+    def keygen_switch(self, sk, s_from, seed=None):
         """Key-switch key from s_from ([L + K, N] NTT form) to sk: (evk_b, evk_a), each
         [dnum, L + K, N] -- the operands of keyswitch / rotate / mul_relin."""
+        seed = _nonce(seed)
         key = _empty(2, self.dnum, self.L + self.K, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_keygen_switch(self._ptr, _ptr(key), _ptr(sk), _ptr(s_from), seed,
                                            _stream(key)), "fhe_keygen_switch")
         return key[0], key[1]
 
-    def keygen_relin(self, sk, seed: int):
+    def keygen_relin(self, sk, seed=None):
         """Relinearisation key: switches s^2 to s."""
         s2 = _empty_like(sk)
         lib = load()
@@ -372,12 +383,13 @@ class Context:
                                   _stream(sk)), "fhe_vec_mul")
         return self.keygen_switch(sk, s2, seed)
 
-    def keygen_rotation(self, sk, galois_elt: int, seed: int):
+    def keygen_rotation(self, sk, galois_elt: int, seed=None):
         """Rotation key for Galois element k: switches sigma_k(s) to s."""
         return self.keygen_switch(sk, self.automorphism(sk, galois_elt, ntt_form=True), seed)
 
-    def encrypt(self, pt, pk, seed: int):
+    def encrypt(self, pt, pk, seed=None):
         """Public-key encryption of an NTT-form plaintext [L, N] -> ciphertext [2, L, N]."""
+        seed = _nonce(seed)
         ct = _empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             ws = self.workspace(self.L * self.n * 8)  # a Graph keeps it (no internal workspace)
@@ -385,7 +397,8 @@ class Context:
                                      _stream(ct)), "fhe_encrypt")
         return ct
 
-    def encrypt_sk(self, pt, sk, seed: int):
+    def encrypt_sk(self, pt, sk, seed=None):
+        seed = _nonce(seed)
         ct = _empty(2, self.L, self.n, dtype=torch.int64, device=self._dev())
         with torch.cuda.device(self.device):
             check(load().fhe_encrypt_sk(self._ptr, _ptr(ct), _ptr(pt), _ptr(sk), seed, _stream(ct)),

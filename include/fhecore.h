@@ -226,7 +226,12 @@ int fhe_deserialize(const fhe_ctx* ctx, const void* host_buf, size_t size, uint6
  * relinearisation, sigma_k(s) for rotation by Galois element k) to s -- the layout fhe_keyswitch,
  * fhe_rotate and fhe_mul_relin take as (evk_b, evk_a).  Ciphertexts [2][L][N] NTT form;
  * plaintexts [L][N] NTT form.  fhe_decrypt: pt = c0 + c1 s over the first nlimbs Q-limbs of
- * `batch` ciphertexts [batch][2][nlimbs][N]. */
+ * `batch` ciphertexts [batch][2][nlimbs][N].
+ * SECURITY: the seed is the whole nonce.  Encryption randomness (u, e0, e1, and a for fhe_encrypt_sk)
+ * and a switch key's a_j are pure functions of (seed, fixed tag), so two encryptions under one key
+ * with the same seed have identical masks (their difference reveals pt1 - pt2), and two switch keys
+ * generated from one seed share a_j.  Never repeat a seed per secret key: draw it from a CSPRNG or
+ * a per-key monotonically increasing counter.  The explicit seed exists so tests are reproducible. */
 int fhe_sample(const fhe_ctx* ctx, uint64_t* out, uint32_t polys, uint32_t limb0,
                uint32_t nlimbs, int kind, uint64_t seed, uint32_t tag, fhe_stream_t stream);
 int fhe_keygen_secret(const fhe_ctx* ctx, uint64_t* sk, uint64_t seed, fhe_stream_t stream);

@@ -124,6 +124,7 @@ struct SwitchKey {
 };
 
 // Counter-based (Philox4x32-10) key generation: every key is a function of (context, seeds).
+// Each seed is a nonce: never reuse one per secret key (see the SECURITY note in fhecore.h).
 class KeyGenerator {
  public:
   KeyGenerator(const Context& ctx, uint64_t seed, hipStream_t stream = nullptr)
