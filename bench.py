@@ -195,7 +195,8 @@ def alu_peaks():
     the kernels' exact forward CT / inverse GS instruction sequences, register-resident, full
     occupancy, no memory traffic), measured once per process on the warmed-up chip."""
     if not _PEAKS:
-        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "microbench", "libbflypeak.so"))
+        lib = ctypes.CDLL(os.environ.get("FHE_PEAK_LIB") or
+                          os.path.join(ROOT, "tools", "microbench", "libbflypeak.so"))
         lib.fhe_peak_bfly.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double)]

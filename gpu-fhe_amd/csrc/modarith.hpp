@@ -80,12 +80,48 @@ __device__ __forceinline__ u64 shoup_fast(u64 y, u64 w, u64 ws, u64 nq) {
   return ((u64)(u32)c << 32) | (u32)t;
 }
 
+// lo32(y1 w0 + y0 w1 + h1 n0 + h0 n1): the four cross terms of a remainder's high word as a chain
+// of v_mad_u64_u32 whose low words carry the sum (the high words are never read), 4 instructions
+// instead of 4 v_mul_lo_u32 + 2 v_add3_u32.  OPAQUE keeps the compiler from shrinking the chain
+// back into mul_lo + add3 (it can see that only the low word is used).  The h terms come last:
+// the chain starts before the quotient is ready.
+__device__ __forceinline__ u32 cross_lo(u32 y0, u32 y1, u32 w0, u32 w1, u32 h0, u32 h1, u32 n0,
+                                        u32 n1) {
+  u64 c = mad_u64_u32(y1, w0, 0);
+  FHE_OPAQUE(c);
+  c = mad_u64_u32(y0, w1, c);
+  FHE_OPAQUE(c);
+  c = mad_u64_u32(h1, n0, c);
+  FHE_OPAQUE(c);
+  c = mad_u64_u32(h0, n1, c);
+  FHE_OPAQUE(c);
+  return (u32)c;
+}
+
+// High word of a remainder: hi32(t) + the cross terms.  CHAIN: the mad chain (one VALU fewer; the
+// issue-bound row kernels); otherwise 4 v_mul_lo_u32 + 2 v_add3_u32, whose independent products
+// carry no back-to-back 64-bit dependences (gfx950 pads each dependent v_mad_u64_u32 pair with a
+// wait state, which costs the latency-bound column passes more than the saved instruction:
+// HomMult column inverse +3 % with the chain).
+template <bool CHAIN>
+__device__ __forceinline__ u32 rem_hi(u64 t, u32 y0, u32 y1, u32 w0, u32 w1, u32 h0, u32 h1,
+                                      u32 n0, u32 n1) {
+  if constexpr (CHAIN) {
+    u32 hi = (u32)(t >> 32) + cross_lo(y0, y1, w0, w1, h0, h1, n0, n1);
+    FHE_OPAQUE(hi);  // one 32-bit add into the high word (not a 64-bit add of a shifted pair)
+    return hi;
+  } else {
+    return (u32)(t >> 32) + y1 * w0 + y0 * w1 + h1 * n0 + h0 * n1;
+  }
+}
+
 // y * w mod q up to two q, any y < 2^64, result in [0, 3q): Shoup with the quotient estimated
 // from three of the four partial products of y * w'.  Dropping hi(y0 s0) (< 2^32 in the 2^32
 // column) lowers h = floor(y w' / 2^64) by at most 1, so r = y w - h q grows by at most q; the
 // 2^32-column sum y1 s0 + y0 s1 may carry into bit 64, which is added back into the high mad.
 // Quotient: 3 mads + 1 select (vs 1 mul_hi + 3 mads + a 64-bit add for the exact one).
 // Remainder: lo64(y w + h nq), nq = -q mod 2^64 (exact: the true value is < 3q).
+template <bool CHAIN = false>
 __device__ __forceinline__ u64 shoup_q3(u64 y, u64 w, u64 ws, u64 nq) {
   const u32 y0 = (u32)y, y1 = (u32)(y >> 32);
   const u32 s0 = (u32)ws, s1 = (u32)(ws >> 32);
@@ -97,18 +133,19 @@ __device__ __forceinline__ u64 shoup_q3(u64 y, u64 w, u64 ws, u64 nq) {
   asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(c) : "s"(cmask));
   const u64 h = mad_u64_u32(y1, s1, ((u64)c << 32) | (u32)(b >> 32));
   // lo64(y w + h nq): the two low-word products as chained mads, the four cross terms only
-  // contribute their low words to the high word (2 mads + 4 mul_lo, no 64-bit add or borrow)
+  // contribute their low words to the high word (rem_hi: a 4-mad chain + 1 add with CHAIN, else
+  // 4 mul_lo + 2 add3; no 64-bit add or borrow either way)
   const u32 w0 = (u32)w, w1 = (u32)(w >> 32), n0 = (u32)nq, n1 = (u32)(nq >> 32);
   const u32 h0 = (u32)h, h1 = (u32)(h >> 32);
   u64 t = mad_u64_u32(h0, n0, (u64)y0 * w0);
   FHE_OPAQUE(t);
-  const u32 hi = (u32)(t >> 32) + y1 * w0 + y0 * w1 + h1 * n0 + h0 * n1;
-  return ((u64)hi << 32) | (u32)t;
+  return ((u64)rem_hi<CHAIN>(t, y0, y1, w0, w1, h0, h1, n0, n1) << 32) | (u32)t;
 }
 
 // u + y * w mod q up to two q (the forward CT butterfly's sum output, shoup_q3 with the X-operand
 // folded in): lo64(u + y w + h nq) -- the addend rides in the first mad of the remainder chain, so
 // the sum costs no separate 64-bit add.  Exact as long as the true value u + (y w - h q) < 2^64.
+template <bool CHAIN = false>
 __device__ __forceinline__ u64 shoup_q3_add(u64 y, u64 w, u64 ws, u64 nq, u64 u) {
   const u32 y0 = (u32)y, y1 = (u32)(y >> 32);
   const u32 s0 = (u32)ws, s1 = (u32)(ws >> 32);
@@ -123,8 +160,7 @@ __device__ __forceinline__ u64 shoup_q3_add(u64 y, u64 w, u64 ws, u64 nq, u64 u)
   const u32 h0 = (u32)h, h1 = (u32)(h >> 32);
   u64 t = mad_u64_u32(h0, n0, mad_u64_u32(y0, w0, u));
   FHE_OPAQUE(t);
-  const u32 hi = (u32)(t >> 32) + y1 * w0 + y0 * w1 + h1 * n0 + h0 * n1;
-  return ((u64)hi << 32) | (u32)t;
+  return ((u64)rem_hi<CHAIN>(t, y0, y1, w0, w1, h0, h1, n0, n1) << 32) | (u32)t;
 }
 
 // a - b + k for a + k > b, with kp1 = k + 1: a + k + 1 + ~b, two 64-bit adds, no borrow chain.
@@ -174,6 +210,68 @@ __device__ __forceinline__ u64 mont_reduce_lazy(u64 tlo, u64 thi, u64 q, u64 qin
 __device__ __forceinline__ u64 mont_redc(u64 tlo, u64 thi, u64 q, u64 qi) {
   const u64 m = tlo * qi;
   return (thi + q) - mulhi64(m, q);
+}
+
+// 128-bit products for the HomMult tensor, operands below 2^61 (forward outputs in [0, 2q), every
+// modulus < 2^60: the lz16 contexts).  Written out as 32x32 partial products so the compiler does
+// not lower a u128 multiply (11 VALU per product with its register-pair moves):
+//   A B = a1 b1 2^64 + (a0 b1 + a1 b0) 2^32 + a0 b0, where a1, b1 < 2^29, so the middle column
+//   (< 2^62; four of them < 2^63) never overflows and only the low column's carries need care.
+__device__ __forceinline__ void mul_wide61(u64 A, u64 B, u64& tlo, u64& thi) {
+  const u32 a0 = (u32)A, a1 = (u32)(A >> 32), b0 = (u32)B, b1 = (u32)(B >> 32);
+  u64 p = mad_u64_u32(a0, b0, 0);
+  FHE_OPAQUE(p);
+  u64 m = mad_u64_u32(a0, b1, 0);
+  FHE_OPAQUE(m);
+  m = mad_u64_u32(a1, b0, m);
+  FHE_OPAQUE(m);
+  u32 c;
+  const u32 th = __builtin_addc((u32)(p >> 32), (u32)m, 0u, &c);
+  thi = mad_u64_u32(a1, b1, (u64)((u32)(m >> 32) + c));
+  tlo = ((u64)th << 32) | (u32)p;
+}
+
+// A B + C D for operands below 2^61 (the tensor's d1): the two low-column products may carry out
+// of 64 bits (captured from the second mad's carry-out), the four middle ones stay below 2^63.
+__device__ __forceinline__ void mul2_wide61(u64 A, u64 B, u64 C, u64 D, u64& tlo, u64& thi) {
+  const u32 a0 = (u32)A, a1 = (u32)(A >> 32), b0 = (u32)B, b1 = (u32)(B >> 32);
+  const u32 c0 = (u32)C, c1 = (u32)(C >> 32), d0 = (u32)D, d1 = (u32)(D >> 32);
+  u64 p = mad_u64_u32(a0, b0, 0);
+  FHE_OPAQUE(p);
+  u64 p2, cm;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(p2), "=s"(cm) : "v"(c0), "v"(d0), "v"(p));
+  u64 m = mad_u64_u32(a0, b1, 0);
+  FHE_OPAQUE(m);
+  m = mad_u64_u32(a1, b0, m);
+  FHE_OPAQUE(m);
+  m = mad_u64_u32(c0, d1, m);
+  FHE_OPAQUE(m);
+  m = mad_u64_u32(c1, d0, m);
+  FHE_OPAQUE(m);
+  u32 cc;
+  asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(cc) : "s"(cm));
+  u32 c;
+  const u32 th = __builtin_addc((u32)(p2 >> 32), (u32)m, 0u, &c);
+  u64 h = mad_u64_u32(a1, b1, (u64)((u32)(m >> 32) + c + cc));  // < 2^31 + 2: no wrap
+  FHE_OPAQUE(h);
+  thi = mad_u64_u32(c1, d1, h);
+  tlo = ((u64)th << 32) | (u32)p2;
+}
+
+// mont_redc with hi64(m q) written out (exactness matters here: an error in it shifts the result
+// by integers, not by multiples of q): hi(m0 q0) + m1 q0 cannot overflow, the m0 q1 column's carry
+// out of 64 bits is captured from the mad and added back into the high mad (6 VALU instead of the
+// compiler's 9 with its register-pair moves).  t < q 2^64; result in (0, 2q).
+__device__ __forceinline__ u64 mont_redc_x(u64 tlo, u64 thi, u64 q, u64 qi) {
+  const u64 m = tlo * qi;
+  const u32 m0 = (u32)m, m1 = (u32)(m >> 32), q0 = (u32)q, q1 = (u32)(q >> 32);
+  const u64 a = mad_u64_u32(m1, q0, (u64)__umulhi(m0, q0));
+  u64 b, cmask;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(b), "=s"(cmask) : "v"(m0), "v"(q1), "v"(a));
+  u32 c;
+  asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(c) : "s"(cmask));
+  const u64 e = mad_u64_u32(m1, q1, ((u64)c << 32) | (u32)(b >> 32));
+  return (thi + q) - e;
 }
 
 // Sum of up to four products y_k h_k with y_k, h_k < 2^61, from 30-bit pieces (lo = v & (2^30 - 1),

@@ -334,7 +334,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         u64 u = reduce ? csubk(x[j], qh) : x[j];
         FHE_OPAQUE(u);  // keeps 2u + 3q one v_lshl_add_u64 (not distributed over the select)
         // u + v straight out of the remainder chain; u - v + 3q = (2u + 3q) - (u + v)
-        u64 s = shoup_q3_add(x[jj], w.x, w.y, nq, u);
+        u64 s = shoup_q3_add<GATHER>(x[jj], w.x, w.y, nq, u);
         FHE_OPAQUE(s);
         x[j] = s;
         u64 t2 = (u << 1) + q3;
@@ -389,27 +389,27 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
     });
   } else {
     // GS: inputs in [0, 3q); sum -> [0, 3q); (u - v + 3q) w -> [0, 3q)
-#pragma unroll
-    for (int b = 0; b < KB; ++b) {
-      const int bitpos = LO + b;
-      const int st = LOGR - 1 - bitpos;
+    static_for<0, KB>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      constexpr int bitpos = LO + b;
+      constexpr int st = LOGR - 1 - bitpos;
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
         const u64 u = x[j], v = x[jj];
         const u64 sum = u + v, dif = u - v + q3;
-        if (FIN == kFinalInv && st == 0) {
+        if constexpr (FIN == kFinalInv && st == 0) {
           // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
-          x[j] = csubk(csubk(shoup_q3(sum, nf0.x, nf0.y, nq), q2), q);
-          x[jj] = csubk(csubk(shoup_q3(dif, nf1.x, nf1.y, nq), q2), q);
+          x[j] = csubk(csubk(shoup_q3<GATHER>(sum, nf0.x, nf0.y, nq), q2), q);
+          x[jj] = csubk(csubk(shoup_q3<GATHER>(dif, nf1.x, nf1.y, nq), q2), q);
         } else {
           const ulonglong2 w = twiddle(b, j, bitpos, st);
           x[j] = csubk(sum, q3);
-          x[jj] = shoup_q3(dif, w.x, w.y, nq);
+          x[jj] = shoup_q3<GATHER>(dif, w.x, w.y, nq);
         }
       }
-    }
+    });
   }
 }
 
@@ -820,7 +820,28 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   // subtractive REDC (mont_redc): no carry-in term, 3 VALU fewer per element than the additive one
   u64 qi = 0 - m.qinv;  // q^-1 mod 2^64
   asm("" : "+s"(qi));
-  if (grp == 1) {
+  if constexpr (HR == 16) {
+    // every modulus < 2^60: operands below 2^61, hand-written partial products and REDC
+    // (d1 -42 %, d0 / d2 -26 % static VALU)
+    if (grp == 1) {
+#pragma unroll
+      for (int j = 0; j < kE; ++j) {
+        const u32 idx = own.idx(tpT | LayT::jpos(j));
+        u64 tlo, thi;
+        mul2_wide61(rowlds[idx], rowlds[3 * G::RS + idx], rowlds[G::RS + idx],
+                    rowlds[2 * G::RS + idx], tlo, thi);
+        v[j] = mont_redc_x(tlo, thi, q, qi);
+      }
+    } else if (active) {
+#pragma unroll
+      for (int j = 0; j < kE; ++j) {
+        const u32 idx = own.idx(tpT | LayT::jpos(j));
+        u64 tlo, thi;
+        mul_wide61(rowlds[aoff + idx], rowlds[boff + idx], tlo, thi);
+        v[j] = mont_redc_x(tlo, thi, q, qi);
+      }
+    }
+  } else if (grp == 1) {
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
       const u32 idx = own.idx(tpT | LayT::jpos(j));
@@ -1429,8 +1450,9 @@ static int hommult_chunk(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u
   return kUnsupported;
 }
 
-// (Two half-batch pipelines on two streams, so one half's memory-bound column passes share the CUs
-// with the other half's VALU-bound fused row kernel, measured no gain: 37.2k vs 36.9k HomMult/s.)
+// (Measured no gain, DESIGN.md §8: two half-batch pipelines on two streams, 37.2k vs 36.9k
+// HomMult/s; chunks of 4-16 ciphertexts so the workspace stays in the Infinity Cache, -1 ... -11 %
+// (launch tails in the column passes); those chunks alternating over two streams, +0.5 %.)
 int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                    u32 nlimbs, void* ws, hipStream_t s) {
   if ((u64)batch * nlimbs == 0) return kOk;

@@ -251,3 +251,83 @@ def test_reduce128_wide_and_wide_tensor(q):
         assert t < q << 64
         r = mont_reduce_lazy(t, q)
         assert 0 <= r < 2 * q and r % q == (t * R_inv) % q
+
+
+def cross_lo_chain(y0, y1, w0, w1, h0, h1, n0, n1):
+    """modarith.hpp cross_lo: four chained v_mad_u64_u32, only the low word read."""
+    c = y1 * w0
+    for a, b in ((y0, w1), (h1, n0), (h0, n1)):
+        c = (a * b + c) & M64
+    return c & M32
+
+
+def test_cross_lo_chain_equals_mul_lo_sum():
+    rng = random.Random(5)
+    for _ in range(20000):
+        v = [rng.getrandbits(32) for _ in range(8)]
+        y0, y1, w0, w1, h0, h1, n0, n1 = v
+        assert cross_lo_chain(*v) == (y1 * w0 + y0 * w1 + h1 * n0 + h0 * n1) & M32
+
+
+def mul_wide61(a, b):
+    """modarith.hpp mul_wide61: a b for a, b < 2^61 from four 32x32 partial products."""
+    a0, a1, b0, b1 = a & M32, a >> 32, b & M32, b >> 32
+    p = a0 * b0
+    m = a0 * b1 + a1 * b0
+    assert m < 1 << 64
+    s = (p >> 32) + (m & M32)
+    th, c = s & M32, s >> 32
+    x = (m >> 32) + c
+    assert x <= M32
+    thi = (a1 * b1 + x) & M64
+    return (thi << 64) | (th << 32) | (p & M32)
+
+
+def mul2_wide61(a, b, c, d):
+    """modarith.hpp mul2_wide61: a b + c d for operands < 2^61 (the tensor's d1)."""
+    a0, a1, b0, b1 = a & M32, a >> 32, b & M32, b >> 32
+    c0, c1, d0, d1 = c & M32, c >> 32, d & M32, d >> 32
+    p = a0 * b0
+    p2full = c0 * d0 + p
+    p2, cm = p2full & M64, p2full >> 64
+    m = a0 * b1 + a1 * b0 + c0 * d1 + c1 * d0
+    assert m < 1 << 64  # the chained mads never wrap
+    s = (p2 >> 32) + (m & M32)
+    th, cc = s & M32, s >> 32
+    x = (m >> 32) + cc + cm
+    assert x <= M32  # the 32-bit addend of the high mad does not wrap
+    thi = (c1 * d1 + a1 * b1 + x) & M64
+    return (thi << 64) | (th << 32) | (p2 & M32)
+
+
+def mont_redc_x(t, q):
+    """modarith.hpp mont_redc_x: subtractive REDC with hi64(m q) from four partial products."""
+    qi = pow(q, -1, 1 << 64)
+    tlo, thi = t & M64, t >> 64
+    m = (tlo * qi) & M64
+    m0, m1, q0, q1 = m & M32, m >> 32, q & M32, q >> 32
+    a = m1 * q0 + ((m0 * q0) >> 32)
+    assert a < 1 << 64
+    bfull = m0 * q1 + a
+    b, c = bfull & M64, bfull >> 64
+    e = (m1 * q1 + ((c << 32) | (b >> 32))) & M64
+    assert e == (m * q) >> 64  # exact, not an estimate
+    return (thi + q - e) & M64
+
+
+@pytest.mark.parametrize("q", [q for q in _moduli() if q < 1 << 60])
+def test_hand_written_tensor(q):
+    """The fused kernel's lz16 tensor: operands in [0, 2q), every q < 2^60; outputs in (0, 2q)."""
+    rng = random.Random(q + 9)
+    R_inv = pow(1 << 64, -1, q)
+    edge = [0, 1, q - 1, q, 2 * q - 1]
+    ops = [(a, b, c, d) for a in edge for b in edge for c in (0, 2 * q - 1) for d in (1, 2 * q - 1)]
+    ops += [tuple(rng.randrange(2 * q) for _ in range(4)) for _ in range(5000)]
+    for a, b, c, d in ops:
+        t1 = mul_wide61(a, b)
+        assert t1 == a * b
+        t2 = mul2_wide61(a, b, c, d)
+        assert t2 == a * b + c * d
+        for t in (t1, t2):
+            r = mont_redc_x(t, q)
+            assert 0 < r < 2 * q and r % q == (t * R_inv) % q

@@ -1,8 +1,9 @@
 // Integer-ALU ceiling for the NTT butterflies (measurement infrastructure for bench.py's
 // `roofline_alu`; not part of libfhecore).
 //
-// Runs the exact butterfly instruction sequences of csrc/ntt.hip round_compute (the lazy forms,
-// lazy, headroom H = 16) on register-resident data at full occupancy, with no memory traffic:
+// Runs the exact butterfly instruction sequences of csrc/ntt.hip round_compute in the row passes
+// (the lazy forms with the mad-chain remainder, shoup_q3<true>; headroom H = 16) on
+// register-resident data at full occupancy, with no memory traffic:
 //   forward  Cooley-Tukey, folded X-operand (shoup_q3_add), the 8q reduction every other stage
 //            (the row passes' schedule), outputs s and (2u + 3q) - s;
 //   inverse  Gentleman-Sande: sum mod 3q, (u - v + 3q) w by shoup_q3.
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(kThreads) void k_bfly_peak(u64* __restrict__ out,
         if constexpr (!INV) {
           u64 u = (b & 1) ? csubk(x[j], 8 * q) : x[j];
           FHE_OPAQUE(u);
-          u64 s = fhe::shoup_q3_add(x[jj], t.x, t.y, nq, u);
+          u64 s = fhe::shoup_q3_add<true>(x[jj], t.x, t.y, nq, u);
           FHE_OPAQUE(s);
           x[j] = s;
           u64 t2 = (u << 1) + q3;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(kThreads) void k_bfly_peak(u64* __restrict__ out,
           const u64 u = x[j], v = x[jj];
           const u64 sum = u + v, dif = u - v + q3;
           x[j] = csubk(sum, q3);
-          x[jj] = fhe::shoup_q3(dif, t.x, t.y, nq);
+          x[jj] = fhe::shoup_q3<true>(dif, t.x, t.y, nq);
         }
       }
     }
