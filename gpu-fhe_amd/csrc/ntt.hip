@@ -646,7 +646,20 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 
   const LViewC<G::SUBS_C> lv{lds + sub};
   const u32 it = blockIdx.x;
   if (it >= items) return;
-  const u32 tile = it % G::TILES_C, pl = it / G::TILES_C;
+  // XCD-grouped placement: workgroups are dealt to the 8 XCDs round-robin, so XCD x takes the
+  // poly-limbs pl = x mod 8 and runs all TILES_C column tiles of one back to back.  Adjacent
+  // 128-byte row segments then come from one XCD close together in time (DRAM page locality):
+  // tools/microbench/colcopy.hip, this access pattern 5.30 -> 5.85 TB/s; with 8 | nlimbs the limb
+  // (and its twiddles) is also tied to the XCD.  Otherwise tiles fastest over all XCDs.
+  u32 tile, pl;
+  if ((items / G::TILES_C) % 8 == 0) {
+    const u32 k = it / 8;
+    tile = k % G::TILES_C;
+    pl = (k / G::TILES_C) * 8 + it % 8;
+  } else {
+    tile = it % G::TILES_C;
+    pl = it / G::TILES_C;
+  }
   const u32 l = pl % nlimbs, p = pl / nlimbs;
   const u64 loc = (u64)l * N + (u64)tile * G::SUBS_C;
   const u64* s = (pm.second(p) ? src2 + pm.src2(p) : src + pm.src(p)) + loc;
