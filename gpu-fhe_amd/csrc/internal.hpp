@@ -84,10 +84,11 @@ namespace fhe {
 int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 polys, u64 pstride,
                u32 limb0, u32 nlimbs, hipStream_t s);
 // the same with separate source / destination poly strides
-// (nfold: the inverse's last-stage fold table [limb][4], default c->d_nfold)
+// (nfold: the inverse's last-stage fold table [limb][4], default c->d_nfold; split: the inverse
+// writes split30(x) -- Sum30's 30-bit pieces -- for k_modup_col, which reads its sources that way)
 int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
                        u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s,
-                       const ulonglong2* nfold = nullptr);
+                       const ulonglong2* nfold = nullptr, bool split = false);
 // Column-forward pass only (first half of a forward NTT; the key-switch's fused row kernel
 // finishes it).
 int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,

@@ -293,12 +293,14 @@ struct Sum30 {
   __device__ __forceinline__ void add(u64 y2, u64 h2) {
     add((u32)y2, (u32)(y2 >> 32), (u32)h2, (u32)(h2 >> 32));
   }
-  __device__ __forceinline__ u64 mont(u64 q, u64 qinv) const {
+  __device__ __forceinline__ u64 mont(u64 q, u64 qinv) const { return csub(mont_lazy(q, qinv), q); }
+  // the same without the final subtraction: [0, 2q)
+  __device__ __forceinline__ u64 mont_lazy(u64 q, u64 qinv) const {
     const u64 a = lo + (mid << 30);
     u64 h = (mid >> 34) + (a < lo ? 1 : 0);
     const u64 l = a + (hi << 60);
     h += (hi >> 4) + (l < a ? 1 : 0);
-    return csub(mont_reduce_lazy(l, h, q, qinv), q);
+    return mont_reduce_lazy(l, h, q, qinv);
   }
 };
 

@@ -121,7 +121,9 @@ struct Layout {
 
 // kFinalFwd reduces the last forward stage to [0, q); kFinalFwd2 only to [0, 2q) (the fused
 // HomMult tensor: its Montgomery products accept operands below 2q).
-enum Final : int { kNotFinal = 0, kFinalFwd = 1, kFinalInv = 2, kFinalFwd2 = 3 };
+// kFinalInvS30: kFinalInv, then each canonical output in Sum30's split form split30(x) (the
+// key-switch's INTTs whose outputs only feed k_modup_col's conversions: it reads them pre-split).
+enum Final : int { kNotFinal = 0, kFinalFwd = 1, kFinalInv = 2, kFinalFwd2 = 3, kFinalInvS30 = 4 };
 
 // LDS exchange fences.  A row sub-transform's threads all sit in one wavefront, so the row
 // kernels only need wavefront-scope ordering of their LDS traffic (DS instructions of one wave
@@ -270,7 +272,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       constexpr int b = TS::T.rep_b[sl];
       constexpr int bitpos = LO + b;
       constexpr int st = LOGR - 1 - bitpos;
-      if constexpr (!(FIN == kFinalInv && st == 0)) {  // the last inverse stage folds N^-1 instead
+      if constexpr (!((FIN == kFinalInv || FIN == kFinalInvS30) && st == 0)) {  // folds N^-1 instead
         // natural group index: g = t W + sj, W = 2^(kElog - bitpos - 1) (the low-bit round has
         // tp = t << kElog); the row tables store those stages lane-major (host_tables.cpp
         // lane_major_rows), so the load index is sj TPS + t and a wavefront reads contiguous words
@@ -399,7 +401,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         const int jj = j | (1 << b);
         const u64 u = x[j], v = x[jj];
         const u64 sum = u + v, dif = u - v + q3;
-        if constexpr (FIN == kFinalInv && st == 0) {
+        if constexpr ((FIN == kFinalInv || FIN == kFinalInvS30) && st == 0) {
           // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
           x[j] = csubk(csubk(shoup_q3<GATHER>(sum, nf0.x, nf0.y, nq), q2), q);
           x[jj] = csubk(csubk(shoup_q3<GATHER>(dif, nf1.x, nf1.y, nq), q2), q);
@@ -410,6 +412,10 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         }
       }
     });
+    if constexpr (FIN == kFinalInvS30) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) x[j] = split30(x[j]);
+    }
   }
 }
 
@@ -634,7 +640,8 @@ struct Geo {
 // (Persistent grids looping over items with a register prefetch of the next one measured slower:
 // vmcnt retires in issue order, so every twiddle wait also waited for the prefetch, and the
 // prefetch registers pushed the column kernel into spills -- DESIGN.md §8.)
-template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false>
+// FI: the inverse's final stage (kFinalInv, or kFinalInvS30 for split30 outputs).
+template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false, int FI = kFinalInv>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_ntt_col(
     const u64* __restrict__ src, const u64* __restrict__ src2, u64* __restrict__ dst, u32 nlimbs,
     u32 limb0, PolyMap pm, u32 items, const ulonglong2* __restrict__ tw_all,
@@ -671,7 +678,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 
     nf0 = nfold[4 * limb];
     nf1 = nfold[4 * limb + 1];
   }
-  pass_run<G::N1, FWD, FWD ? kNotFinal : kFinalInv, kBlockSync, false, H, 1>(
+  pass_run<G::N1, FWD, FWD ? kNotFinal : FI, kBlockSync, false, H, 1>(
       x, GView<G::R2, false, NTS>{dst + pm.dst(p) + loc, sub}, lv, t, tw_all + (u64)limb * N, 1u,
       mods[limb].q, nf0, nf1);
 }
@@ -959,10 +966,10 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
     Sum30 acc;
 #pragma unroll
-    for (int k = 0; k < S; ++k) acc.add(split30(yb[yoff.o[k] + i]), h2[k]);
-    x[j] = acc.mont(m.q, m.qinv);
+    for (int k = 0; k < S; ++k) acc.add(yb[yoff.o[k] + i], h2[k]);  // sources arrive pre-split
+    x[j] = acc.mont_lazy(m.q, m.qinv);  // [0, 2q): the pass takes inputs below 2q
   }
-  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 1>(
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2>(
       x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
       tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
 }
@@ -1036,7 +1043,8 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   const FinishView fo{(h ? ks1 : ks0) + ((u64)b * nq + l) * N + rloc,
                       acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc, lane, q,
                       pinv[limb]};
-  pass_run<G::N2, true, kFinalFwd, kWaveSync, true, H, fwd_range(1, G::N1, H), true>(
+  // column-passed by k_modup_col (inputs below 2q) or k_ntt_col (below q)
+  pass_run<G::N2, true, kFinalFwd, kWaveSync, true, H, fwd_range(2, G::N1, H), true>(
       x, fo, lv, t, tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, q, {0, 0}, {0, 0});
 }
 
@@ -1115,7 +1123,8 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
         constexpr int k = decltype(kc)::value;
         constexpr int KB = Rd::kb(k);
         constexpr int LO = Rd::lo_fwd(k);
-        constexpr int RIN = fwd_range(fwd_range(1, G::N1, HR), G::N2 - (LO + KB), HR);
+        // column-passed by k_modup_col (inputs below 2q: mont_lazy) or k_ntt_col (below q)
+        constexpr int RIN = fwd_range(fwd_range(2, G::N1, HR), G::N2 - (LO + KB), HR);
         using Lay = Layout<G::N2, KB, LO>;
         const u32 tp = Lay::tpos(t);
         if constexpr (k == 0) {
@@ -1208,7 +1217,7 @@ void row_pass(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 
 template <int LOGN, int HD>
 int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* dst,
                  u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s,
-                 const ulonglong2* nfold) {
+                 const ulonglong2* nfold, bool split) {
   using G = Geo<LOGN>;
   const u64 pl = (u64)polys * nlimbs;
   const PolyMap pm{1, spstride, 0, dpstride, 0, 0};
@@ -1226,10 +1235,24 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   } else {
     row_pass<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_inv");
+    const ulonglong2* nf = nfold ? nfold : c->d_nfold;
+    if constexpr (HD != 2) {
+      if (split) {  // outputs for k_modup_col only (narrow contexts: split30 needs x < 2^61)
+        k_ntt_col<LOGN, false, inv_h(HD), false, false, kFinalInvS30>
+            <<<item_grid(ic), G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic,
+                                                c->d_tw_inv, nf, c->d_mods);
+        prof_mark(s, "ntt_col_inv");
+        FHE_HIP_CHECK(hipGetLastError());
+        return kOk;
+      }
+    } else if (split) {
+      set_error("split30 INTT outputs need every modulus < 2^61");
+      return kUnsupported;
+    }
     k_ntt_col<LOGN, false, inv_h(HD)>
         <<<item_grid(ic),
-           G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv,
-                             nfold ? nfold : c->d_nfold, c->d_mods);
+           G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic, c->d_tw_inv, nf,
+                             c->d_mods);
     prof_mark(s, "ntt_col_inv");
   }
   FHE_HIP_CHECK(hipGetLastError());
@@ -1426,17 +1449,17 @@ int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 pol
 
 int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
                        u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s,
-                       const ulonglong2* nfold) {
+                       const ulonglong2* nfold, bool split) {
   if ((u64)polys * nlimbs == 0) return kOk;
   switch (c->log_n) {
 #define X(n) \
   case n:    \
     return c->wide   ? ntt_dispatch<n, 2>(c, forward, src, spstride, dst, dpstride, polys, limb0, \
-                                          nlimbs, s, nfold)                                     \
+                                          nlimbs, s, nfold, split)                              \
            : c->lz16 ? ntt_dispatch<n, 16>(c, forward, src, spstride, dst, dpstride, polys, limb0, \
-                                           nlimbs, s, nfold)                                    \
+                                           nlimbs, s, nfold, split)                             \
                      : ntt_dispatch<n, 8>(c, forward, src, spstride, dst, dpstride, polys, limb0,  \
-                                          nlimbs, s, nfold);
+                                          nlimbs, s, nfold, split);
     FHE_LOGN_CASES(X)
 #undef X
   }

@@ -214,8 +214,9 @@ __global__ __launch_bounds__(kThreads) void k_modup_scale(const u64* __restrict_
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   const u64 q = mods[mod0 + k].q;
   const ulonglong2 w = inv[k];
+  // split30: k_modup_col reads its sources as Sum30 pieces
   y[((u64)b * S + k) * n + i] =
-      csub(shoup_lazy(in[(u64)b * in_bs + koff.o[k] + i], w.x, w.y, q), q);
+      split30(csub(shoup_lazy(in[(u64)b * in_bs + koff.o[k] + i], w.x, w.y, q), q));
 }
 
 // host Shoup-pair table -> device ulonglong2 array (same 16-byte layout)
@@ -468,7 +469,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     // folds N^-1 (P^_k)^-1, c->d_nfold_down): no separate scaling pass
     u64* ydn = ext;
     if ((rc = launch_ntt_strided(c, false, accp, rn, ydn, (u64)K * n, 2 * batch, L, K, s,
-                                 c->d_nfold_down)))
+                                 c->d_nfold_down, true)))
       return rc;
     prof_mark(s, "ks_moddown_conv");
     const ModUpColArgs md{ydn, (u64)K * n, {0, n, 2 * n, 3 * n}, conv, (u64)nlimbs * n, K, nlimbs,
