@@ -258,6 +258,44 @@ __device__ __forceinline__ void mul2_wide61(u64 A, u64 B, u64 C, u64 D, u64& tlo
   tlo = ((u64)th << 32) | (u32)p2;
 }
 
+// sum_d x_d k_d (D <= 4 terms) as a 128-bit (tlo, thi) for x_d, k_d < 2^61 with k_d < 2^60 (the
+// key-switch inner product of an lz16 context: row-forward outputs reduced below 2q, key residues
+// below q).  The middle column (2D products < 2^61 each) stays below 2^64, the high one far below;
+// the low column's carries are counted straight from the mads' carry-outs (v_addc with the carry
+// SGPR as carry-in).  24 VALU for D = 4 where the compiler's u128 lowering takes 55.
+template <int D>
+__device__ __forceinline__ void dot_wide61(const u64 (&x)[D], const u64 (&k)[D], u64& tlo,
+                                           u64& thi) {
+  u64 l = mad_u64_u32((u32)x[0], (u32)k[0], 0);
+  FHE_OPAQUE(l);
+  u32 carries = 0;
+#pragma unroll
+  for (int d = 1; d < D; ++d) {
+    u64 nl, cm, dead;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(nl), "=s"(cm) : "v"((u32)x[d]), "v"((u32)k[d]), "v"(l));
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(carries), "=s"(dead) : "v"(carries), "s"(cm));
+    l = nl;
+  }
+  u64 m = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    m = mad_u64_u32((u32)x[d], (u32)(k[d] >> 32), m);
+    FHE_OPAQUE(m);
+    m = mad_u64_u32((u32)(x[d] >> 32), (u32)k[d], m);
+    FHE_OPAQUE(m);
+  }
+  u32 c;
+  const u32 th = __builtin_addc((u32)(l >> 32), (u32)m, 0u, &c);
+  u64 h = (u64)((u32)(m >> 32) + c + carries);  // m < 1.5 2^63: no 32-bit wrap
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    h = mad_u64_u32((u32)(x[d] >> 32), (u32)(k[d] >> 32), h);
+    FHE_OPAQUE(h);
+  }
+  thi = h;
+  tlo = ((u64)th << 32) | (u32)l;
+}
+
 // mont_redc with hi64(m q) written out (exactness matters here: an error in it shifts the result
 // by integers, not by multiples of q): hi(m0 q0) + m1 q0 cannot overflow, the m0 q1 column's carry
 // out of 64 bits is captured from the mad and added back into the high mad (6 VALU instead of the

@@ -1134,8 +1134,9 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
           lds_sync<SY>();
           own_slot.template load<Lay>(v, tp);
         }
-        round_compute<G::N2, KB, LO, true, kNotFinal, true, HR, RIN>(v, tp, tf, base, q, {0, 0},
-                                                                     {0, 0});
+        // lz16: the last round reduces to [0, 2q) for the hand-written inner product (dot_wide61)
+        constexpr int F = (HR == 16 && k == Rd::NR - 1) ? kFinalFwd2 : kNotFinal;
+        round_compute<G::N2, KB, LO, true, F, true, HR, RIN>(v, tp, tf, base, q, {0, 0}, {0, 0});
         if constexpr (k < Rd::NR - 1) {
           if (k > 0) lds_sync<SY>();
           own_slot.template store<Lay>(v, tp);
@@ -1156,6 +1157,33 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
   const u64 okey = (u64)r * N + (u64)(tile * H::ROWS + crow) * G::R2 + cpos;
   const u64* lrow = lds + crow * H::ROWW;
   u64 o0[CW], o1[CW];
+  if constexpr (HR == 16) {
+#pragma unroll
+    for (int e = 0; e < CW; e += 2) {
+      u64 x0[DNUM], x1[DNUM], kb0[DNUM], kb1[DNUM], ka0[DNUM], ka1[DNUM];
+#pragma unroll
+      for (int d = 0; d < DNUM; ++d) {
+        const u64x2_t kb = *(const __attribute__((address_space(1))) u64x2_t*)(evk_b + (u64)d * rn + okey + e);
+        const u64x2_t ka = *(const __attribute__((address_space(1))) u64x2_t*)(evk_a + (u64)d * rn + okey + e);
+        const u32 p = cpos + e;
+        x0[d] = lrow[d * G::RS + p + (p >> 4)];
+        x1[d] = lrow[d * G::RS + (p + 1) + ((p + 1) >> 4)];
+        kb0[d] = kb.x;
+        kb1[d] = kb.y;
+        ka0[d] = ka.x;
+        ka1[d] = ka.y;
+      }
+      u64 tl, th;
+      dot_wide61<DNUM>(x0, kb0, tl, th);
+      o0[e] = reduce128(tl, th, m);
+      dot_wide61<DNUM>(x1, kb1, tl, th);
+      o0[e + 1] = reduce128(tl, th, m);
+      dot_wide61<DNUM>(x0, ka0, tl, th);
+      o1[e] = reduce128(tl, th, m);
+      dot_wide61<DNUM>(x1, ka1, tl, th);
+      o1[e + 1] = reduce128(tl, th, m);
+    }
+  } else {
 #pragma unroll
   for (int e = 0; e < CW; e += 2) {
     u128 s0[2] = {0, 0}, s1[2] = {0, 0};
@@ -1176,6 +1204,7 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
       o0[e + h] = reduce128((u64)s0[h], (u64)(s0[h] >> 64), m);
       o1[e + h] = reduce128((u64)s1[h], (u64)(s1[h] >> 64), m);
     }
+  }
   }
   gptr_u128 a0 = (gptr_u128)(acc + (u64)b * rn + okey);
   gptr_u128 a1 = (gptr_u128)(acc + acc_ws + (u64)b * rn + okey);

@@ -331,3 +331,33 @@ def test_hand_written_tensor(q):
         for t in (t1, t2):
             r = mont_redc_x(t, q)
             assert 0 < r < 2 * q and r % q == (t * R_inv) % q
+
+
+def dot_wide61(xs, ks):
+    """modarith.hpp dot_wide61: sum of D <= 4 products x k (x < 2^61, k < 2^60) as 128 bits."""
+    lo = (xs[0] & M32) * (ks[0] & M32)
+    carries = 0
+    for x, k in zip(xs[1:], ks[1:]):
+        full = (x & M32) * (k & M32) + lo
+        lo, carries = full & M64, carries + (full >> 64)
+    m = sum((x & M32) * (k >> 32) + (x >> 32) * (k & M32) for x, k in zip(xs, ks))
+    assert m < 1 << 64
+    s = (lo >> 32) + (m & M32)
+    th, c = s & M32, s >> 32
+    h = (m >> 32) + c + carries
+    assert h <= M32  # the 32-bit addend of the high chain does not wrap
+    for x, k in zip(xs, ks):
+        h = ((x >> 32) * (k >> 32) + h) & M64
+    return (h << 64) | (th << 32) | (lo & M32)
+
+
+@pytest.mark.parametrize("q", [q for q in _moduli() if q < 1 << 60])
+def test_keyswitch_inner_product_dot(q):
+    """k_ks_row_inner's lz16 combine: row outputs in [0, 2q), key residues in [0, q)."""
+    rng = random.Random(q + 11)
+    for D in (1, 2, 3, 4):
+        cases = [([2 * q - 1] * D, [q - 1] * D), ([0] * D, [0] * D)]
+        cases += [([rng.randrange(2 * q) for _ in range(D)], [rng.randrange(q) for _ in range(D)])
+                  for _ in range(3000)]
+        for xs, ks in cases:
+            assert dot_wide61(xs, ks) == sum(x * k for x, k in zip(xs, ks))
