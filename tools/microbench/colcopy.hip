@@ -31,6 +31,25 @@ __global__ __launch_bounds__(T) void k_colcopy(const u64* __restrict__ src, u64*
   for (int j = 0; j < E; ++j) dst[base + (u64)(t + j * STEP) * R] = x[j] + 1;
 }
 
+// TPW tiles per workgroup, one after another (XCD-grouped as above): fewer, longer workgroups.
+template <int TPW>
+__global__ __launch_bounds__(256) void k_colcopy_loop(const u64* __restrict__ src, u64* dst) {
+  constexpr int R = 256, W = 16, E = 16, STEP = 16, tiles = R / W;
+  const int col = threadIdx.x % W, t = threadIdx.x / W;
+  const int x = blockIdx.x % 8, k = blockIdx.x / 8;
+#pragma unroll 1
+  for (int i = 0; i < TPW; ++i) {
+    const int kk = k * TPW + i;
+    const int tile = kk % tiles, p = (kk / tiles) * 8 + x;
+    const u64 base = (u64)p * R * R + (u64)tile * W + col;
+    u64 v[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = src[base + (u64)(t + j * STEP) * R];
+#pragma unroll
+    for (int j = 0; j < E; ++j) dst[base + (u64)(t + j * STEP) * R] = v[j] + 1;
+  }
+}
+
 __global__ void k_linear(const ulonglong2* __restrict__ s, ulonglong2* d, u64 n2) {
   for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n2; i += (u64)gridDim.x * blockDim.x) {
     ulonglong2 v = s[i];
@@ -79,6 +98,12 @@ int main() {
   RUNX(32, 512, false, true, d, "W=32 T=512 XCD-grouped")
   RUNX(32, 256, false, true, d, "W=32 T=256 XCD-grouped")
   RUN(16, 256, false, d, "W=16 T=256 (shipped) again")
+  printf("%-28s %6.0f GB/s\n", "XCD-grouped, 2 tiles/WG",
+         bytes / timeit([&] { k_colcopy_loop<2><<<polys * 16 / 2, 256>>>(s, d); }) / 1e6);
+  printf("%-28s %6.0f GB/s\n", "XCD-grouped, 4 tiles/WG",
+         bytes / timeit([&] { k_colcopy_loop<4><<<polys * 16 / 4, 256>>>(s, d); }) / 1e6);
+  printf("%-28s %6.0f GB/s\n", "XCD-grouped, 16 tiles/WG",
+         bytes / timeit([&] { k_colcopy_loop<16><<<polys * 16 / 16, 256>>>(s, d); }) / 1e6);
   printf("%-28s %6.0f GB/s\n", "linear copy",
          bytes / timeit([&] { k_linear<<<8192, 256>>>((ulonglong2*)s, (ulonglong2*)d, words / 2); }) / 1e6);
   return 0;
