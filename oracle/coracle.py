@@ -52,6 +52,9 @@ def lib():
             f.restype = None
         L.port_hommult.argtypes = [_u64p, _u64p, _u64p, u64, u32, _u64p, u32]
         L.port_hommult.restype = None
+        L.port_keyswitch.argtypes = [_u64p, _u64p, _u64p, _u64p, _u64p, u64, u32, _u64p, u32,
+                                     _u64p, u32, u32]
+        L.port_keyswitch.restype = None
         _lib = L
     return _lib
 
@@ -165,6 +168,19 @@ def baseconv(x, src, dst) -> np.ndarray:
     out = np.empty((dst.size, n), dtype=np.uint64)
     lib().oracle_baseconv(_p(out), _p(x), n, _p(src), src.size, _p(dst), dst.size)
     return out
+
+
+def port_keyswitch(d2, evk_b, evk_a, qs, ps, dnum):
+    """The tuned CPU port's key-switch (oracle/fhe_cpu_port.c): d2 [batch][L][N] -> (ks0, ks1)."""
+    d2 = _u64(d2)
+    B, L, n = d2.shape
+    qs = _u64(qs)
+    ps = _u64(ps)
+    ks0 = np.empty((B, L, n), dtype=np.uint64)
+    ks1 = np.empty((B, L, n), dtype=np.uint64)
+    lib().port_keyswitch(_p(ks0), _p(ks1), _p(d2), _p(_u64(evk_b)), _p(_u64(evk_a)), B,
+                         n.bit_length() - 1, _p(qs), qs.size, _p(ps), ps.size, dnum)
+    return ks0, ks1
 
 
 def keyswitch(d2, evk_b, evk_a, qs, ps, dnum):

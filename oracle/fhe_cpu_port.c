@@ -220,3 +220,177 @@ void port_hommult(u64* d, const u64* a, const u64* b, uint64_t batch, uint32_t l
     free(s);
   }
 }
+
+/* ---------------------------------------------------------------- hybrid key-switch (port)
+ * The same algorithm as oracle_keyswitch (SURVEY.md §8a'; INTT d2 -> per digit ModUp + NTT ->
+ * inner product with the key -> ModDown), written like a tuned CPU library: cached twiddle tables,
+ * lazy Harvey NTTs, Shoup products for every constant factor, 128-bit sums reduced once by two
+ * Shoup products (no `%`), one scratch row + two 128-bit accumulator rows per OpenMP thread, and
+ * the batch's key shared.  d2, ks0, ks1 [batch][L][N] NTT form; evk_b, evk_a [dnum][L+K][N]. */
+
+typedef struct { u64 q, r64, r64s, one_s; } red_t;  /* 2^64 mod q and its / 1's Shoup companions */
+
+static red_t red_make(u64 q) {
+  red_t r;
+  r.q = q;
+  r.r64 = (u64)(((u128)1 << 64) % q);
+  r.r64s = shoup_c(r.r64, q);
+  r.one_s = shoup_c(1, q);
+  return r;
+}
+
+/* any 128-bit z mod q (q < 2^62): z_hi (2^64 mod q) + z_lo, each Shoup product in [0, 2q) */
+static inline u64 red128(u128 z, const red_t* r) {
+  const u64 q = r->q;
+  u64 s = shoup((u64)(z >> 64), r->r64, r->r64s, q) + shoup((u64)z, 1, r->one_s, q);
+  s = s >= 2 * q ? s - 2 * q : s;
+  return s >= q ? s - q : s;
+}
+
+/* canonical x c mod q for a constant c with Shoup companion cs */
+static inline u64 mulc(u64 x, u64 c, u64 cs, u64 q) {
+  const u64 r = shoup(x, c, cs, q);
+  return r >= q ? r - q : r;
+}
+
+void port_keyswitch(u64* ks0, u64* ks1, const u64* d2, const u64* evk_b, const u64* evk_a,
+                    uint64_t batch, uint32_t log_n, const u64* qs, uint32_t L, const u64* ps,
+                    uint32_t K, uint32_t dnum) {
+  const u64 n = 1ull << log_n;
+  const uint32_t LK = L + K, alpha = (L + dnum - 1) / dnum;
+  u64* mods = malloc(LK * 8);
+  memcpy(mods, qs, L * 8);
+  memcpy(mods + L, ps, K * 8);
+  prepare(log_n, mods, LK);
+  red_t* red = malloc(LK * sizeof(red_t));
+  for (uint32_t i = 0; i < LK; ++i) red[i] = red_make(mods[i]);
+  /* ModUp constants: limb l of digit j = l / alpha: (D^_l)^-1 mod q_l, and D^_l mod m_t */
+  u64* uinv = malloc(L * 8);
+  u64* uinvs = malloc(L * 8);
+  u64* uhat = malloc((u64)L * LK * 8);
+  for (uint32_t l = 0; l < L; ++l) {
+    const uint32_t lo = l / alpha * alpha, hi = lo + alpha < L ? lo + alpha : L;
+    u64 h = 1;
+    for (uint32_t k = lo; k < hi; ++k)
+      if (k != l) h = mulmod(h, qs[k] % qs[l], qs[l]);
+    uinv[l] = powmod(h, qs[l] - 2, qs[l]);
+    uinvs[l] = shoup_c(uinv[l], qs[l]);
+    for (uint32_t t = 0; t < LK; ++t) {
+      u64 hm = 1;
+      for (uint32_t k = lo; k < hi; ++k)
+        if (k != l) hm = mulmod(hm, qs[k] % mods[t], mods[t]);
+      uhat[(u64)l * LK + t] = hm;
+    }
+  }
+  /* ModDown constants: (P^_k)^-1 mod p_k, P^_k mod q_i, P^-1 mod q_i */
+  u64 dinv[64], dinvs[64], pinv[64], pinvs[64];
+  u64* dhat = malloc((u64)K * L * 8);
+  for (uint32_t k = 0; k < K; ++k) {
+    u64 h = 1;
+    for (uint32_t m = 0; m < K; ++m)
+      if (m != k) h = mulmod(h, ps[m] % ps[k], ps[k]);
+    dinv[k] = powmod(h, ps[k] - 2, ps[k]);
+    dinvs[k] = shoup_c(dinv[k], ps[k]);
+    for (uint32_t i = 0; i < L; ++i) {
+      u64 hm = 1;
+      for (uint32_t m = 0; m < K; ++m)
+        if (m != k) hm = mulmod(hm, ps[m] % qs[i], qs[i]);
+      dhat[(u64)k * L + i] = hm;
+    }
+  }
+  for (uint32_t i = 0; i < L; ++i) {
+    u64 pm = 1;
+    for (uint32_t k = 0; k < K; ++k) pm = mulmod(pm, ps[k] % qs[i], qs[i]);
+    pinv[i] = powmod(pm, qs[i] - 2, qs[i]);
+    pinvs[i] = shoup_c(pinv[i], qs[i]);
+  }
+  u64* y = malloc((u64)L * n * 8);          /* ModUp sources [L][N] */
+  u64* acc = malloc((u64)2 * LK * n * 8);  /* [2][LK][N] */
+  u64* yp = malloc((u64)2 * K * n * 8);    /* ModDown sources [2][K][N] */
+  for (u64 b = 0; b < batch; ++b) {
+    const u64* d2b = d2 + b * L * n;
+#pragma omp parallel for schedule(dynamic)
+    for (int64_t l = 0; l < (int64_t)L; ++l) {
+      const ptab_t* t = ptab(qs[l], log_n);
+      u64* yl = y + (u64)l * n;
+      memcpy(yl, d2b + (u64)l * n, n * 8);
+      port_inv_1(yl, t, t->ninv, t->ninvs);
+      for (u64 k = 0; k < n; ++k) yl[k] = mulc(yl[k], uinv[l], uinvs[l], qs[l]);
+    }
+#pragma omp parallel
+    {
+      u64* row = malloc(n * 8);
+      u128* s0 = malloc(n * sizeof(u128));
+      u128* s1 = malloc(n * sizeof(u128));
+#pragma omp for schedule(dynamic)
+      for (int64_t i = 0; i < (int64_t)LK; ++i) {
+        const ptab_t* t = ptab(mods[i], log_n);
+        memset(s0, 0, n * sizeof(u128));
+        memset(s1, 0, n * sizeof(u128));
+        for (uint32_t j = 0; j < dnum; ++j) {
+          const uint32_t lo = j * alpha, hi = lo + alpha < L ? lo + alpha : L;
+          if (lo >= L) break;
+          const u64* x;
+          if (i >= (int64_t)lo && i < (int64_t)hi) {
+            x = d2b + (u64)i * n; /* the digit's own limb: d2 itself (NTT form) */
+          } else {
+            for (u64 k = 0; k < n; ++k) {
+              u128 z = 0;
+              for (uint32_t l = lo; l < hi; ++l) z += (u128)y[(u64)l * n + k] * uhat[(u64)l * LK + i];
+              row[k] = red128(z, &red[i]);
+            }
+            port_fwd_1(row, t);
+            x = row;
+          }
+          const u64* eb = evk_b + ((u64)j * LK + i) * n;
+          const u64* ea = evk_a + ((u64)j * LK + i) * n;
+          for (u64 k = 0; k < n; ++k) {
+            s0[k] += (u128)x[k] * eb[k];
+            s1[k] += (u128)x[k] * ea[k];
+          }
+        }
+        u64* a0 = acc + (u64)i * n;
+        u64* a1 = acc + ((u64)LK + i) * n;
+        for (u64 k = 0; k < n; ++k) {
+          a0[k] = red128(s0[k], &red[i]);
+          a1[k] = red128(s1[k], &red[i]);
+        }
+      }
+      free(row); free(s0); free(s1);
+    }
+    /* ModDown both accumulators: INTT + scale of the P rows, then per Q-limb convert, NTT, finish */
+#pragma omp parallel for schedule(dynamic)
+    for (int64_t hk = 0; hk < (int64_t)(2 * K); ++hk) {
+      const uint32_t h = (uint32_t)hk / K, k = (uint32_t)hk % K;
+      const ptab_t* t = ptab(ps[k], log_n);
+      u64* x = yp + (u64)hk * n;
+      memcpy(x, acc + ((u64)h * LK + L + k) * n, n * 8);
+      port_inv_1(x, t, t->ninv, t->ninvs);
+      for (u64 m = 0; m < n; ++m) x[m] = mulc(x[m], dinv[k], dinvs[k], ps[k]);
+    }
+#pragma omp parallel
+    {
+      u64* row = malloc(n * 8);
+#pragma omp for schedule(dynamic)
+      for (int64_t hi_ = 0; hi_ < (int64_t)(2 * L); ++hi_) {
+        const uint32_t h = (uint32_t)hi_ / L, i = (uint32_t)hi_ % L;
+        const ptab_t* t = ptab(qs[i], log_n);
+        const u64 q = qs[i];
+        for (u64 m = 0; m < n; ++m) {
+          u128 z = 0;
+          for (uint32_t k = 0; k < K; ++k) z += (u128)yp[((u64)h * K + k) * n + m] * dhat[(u64)k * L + i];
+          row[m] = red128(z, &red[i]);
+        }
+        port_fwd_1(row, t);
+        const u64* a = acc + ((u64)h * LK + i) * n;
+        u64* out = (h ? ks1 : ks0) + (b * L + i) * n;
+        for (u64 m = 0; m < n; ++m) {
+          const u64 x = a[m], v = row[m];
+          out[m] = mulc(x >= v ? x - v : x + q - v, pinv[i], pinvs[i], q);
+        }
+      }
+      free(row);
+    }
+  }
+  free(mods); free(red); free(uinv); free(uinvs); free(uhat); free(dhat); free(y); free(acc); free(yp);
+}

@@ -272,3 +272,23 @@ def test_cpu_port_matches_oracle(log_n, bits):
     a = np.stack([rng.integers(0, q, (2, 2, n), dtype=np.uint64) for q in mods], axis=2)
     b = np.stack([rng.integers(0, q, (2, 2, n), dtype=np.uint64) for q in mods], axis=2)
     assert (coracle.port_hommult(a, b, mods) == coracle.hommult(a, b, mods)).all()
+
+
+@pytest.mark.parametrize("log_n,L,K,dnum", [(10, 4, 2, 2), (11, 5, 2, 3), (10, 6, 3, 6), (12, 16, 4, 4)])
+def test_cpu_port_keyswitch_matches_oracle(log_n, L, K, dnum):
+    """The tuned key-switch port (bench.py's key-switch cpu_baseline) equals the exact checker."""
+    import coracle
+
+    allm = coracle.gen_moduli(log_n, L + K)
+    qs, ps = allm[:L], allm[L:]
+    rng = np.random.default_rng(log_n * 7 + L)
+    n = 1 << log_n
+    B = 2
+    d2 = np.stack([rng.integers(0, q, (B, n), dtype=np.uint64) for q in qs], axis=1)
+    d2[0, :, :4] = np.asarray(qs, dtype=np.uint64)[:, None] - 1
+    eb = np.stack([rng.integers(0, q, (dnum, n), dtype=np.uint64) for q in allm], axis=1)
+    ea = np.stack([rng.integers(0, q, (dnum, n), dtype=np.uint64) for q in allm], axis=1)
+    k0, k1 = coracle.port_keyswitch(d2, eb, ea, qs, ps, dnum)
+    for b in range(B):
+        r0, r1 = coracle.keyswitch(d2[b], eb, ea, qs, ps, dnum)
+        assert (k0[b] == r0).all() and (k1[b] == r1).all()
