@@ -90,3 +90,13 @@ def test_no_cpu_fallback_without_device():
         arithmetic.vec_add(np.zeros(4, np.uint64), np.zeros(4, np.uint64), 7)
     with pytest.raises(fhecore.FheError):
         arithmetic.NTT(np.zeros(4096, np.uint64))
+
+
+def test_keygen_seed_defaults_to_fresh_nonce():
+    """Python keygen / encryption draw a fresh 64-bit CSPRNG seed when none is given (seeds are
+    nonces: fhecore.h SECURITY note); an explicit seed is passed through unchanged."""
+    from fhecore import context
+
+    drawn = {context._nonce(None) for _ in range(64)}
+    assert len(drawn) == 64 and all(0 <= s < 1 << 64 for s in drawn)
+    assert context._nonce(7) == 7
