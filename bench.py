@@ -70,9 +70,16 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    # FHE_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU (the
+    # driver's runs use RCCL, one rank per GPU)
+    backend = os.environ.get("FHE_BENCH_BACKEND", "nccl")
+    dev = local % torch.cuda.device_count() if backend != "nccl" else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            torch.distributed.init_process_group(backend)
     return world, rank
 
 
@@ -85,7 +92,8 @@ def barrier(world):
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    nccl = torch.distributed.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if nccl else "cpu")
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return float(t.item())
 
