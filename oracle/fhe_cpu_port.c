@@ -257,6 +257,7 @@ void port_keyswitch(u64* ks0, u64* ks1, const u64* d2, const u64* evk_b, const u
                     uint64_t batch, uint32_t log_n, const u64* qs, uint32_t L, const u64* ps,
                     uint32_t K, uint32_t dnum) {
   const u64 n = 1ull << log_n;
+  if (L == 0 || K == 0 || dnum == 0 || L > 64 || K > 64) return; /* the constant tables below */
   const uint32_t LK = L + K, alpha = (L + dnum - 1) / dnum;
   u64* mods = malloc(LK * 8);
   memcpy(mods, qs, L * 8);
