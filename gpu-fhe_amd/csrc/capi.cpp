@@ -261,7 +261,7 @@ int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t
   // a prepared input when the fused ModUp applies: the INTT folds (D^_k)^-1 into its last stage
   const bool prep = ks_prepared(c);
   if ((rc = launch_ntt_strided(c, false, d2, (uint64_t)c->L * c->n, c_all, (uint64_t)c->L * c->n,
-                               batch, 0, c->L, hs(s), prep ? c->d_nfold_up : nullptr, prep)))
+                               batch, 0, c->L, hs(s), prep ? c->d_nfold_up : nullptr, prep && ks_split30(c))))
     return rc;
   CAll src = CAll::contiguous(c_all, c->L, c->n);
   src.scaled = prep;

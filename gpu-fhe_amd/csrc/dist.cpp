@@ -181,7 +181,8 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
     if (nl && bn &&
         (rc = launch_ntt_strided(ctx, false, d2_own + (u64)b0 * nl * n, (u64)nl * n,
                                  gbuf + (u64)r * blk, (u64)cw * n, bn, limb0, nl, s,
-                                 prep ? ctx->d_nfold_up : nullptr, prep)))
+                                 prep ? ctx->d_nfold_up : nullptr,
+                                 prep && ks_split30(ctx))))
       return rc;
     FHE_HIP_CHECK(hipEventRecord(comm->ev_intt[k], s));
     FHE_HIP_CHECK(hipStreamWaitEvent(comm->stream, comm->ev_intt[k], 0));

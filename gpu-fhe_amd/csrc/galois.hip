@@ -243,7 +243,7 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
   u64* c_all = reinterpret_cast<u64*>(reinterpret_cast<char*>(kws) + kbytes) - batch * ln;
   const bool prep = ks_prepared(c);  // the INTT emits ModUp's scaled inputs
   if ((rc = launch_ntt_strided(c, false, sc1, ln, c_all, ln, batch, 0, L, s,
-                               prep ? c->d_nfold_up : nullptr, prep)))
+                               prep ? c->d_nfold_up : nullptr, prep && ks_split30(c))))
     return rc;
   CAll call = CAll::contiguous(c_all, L, n);
   call.scaled = prep;

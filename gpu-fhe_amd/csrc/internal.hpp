@@ -183,6 +183,10 @@ struct CAll {
 inline bool ks_prepared(const fhe_ctx* c) {
   return c->K > 0 && c->dnum <= 4 && c->alpha <= 4 && !c->wide;
 }
+// The fused conversions' source format (k_modup_col): lz16 contexts (every q < 2^60) read plain
+// residues (dot_wide61 on 32-bit halves); the others read Sum30's 30-bit pieces (split30), which
+// the INTTs and k_modup_scale feeding them emit directly.
+inline bool ks_split30(const fhe_ctx* c) { return !c->lz16; }
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
                            u32 nlimbs, u32 batch, void* ws, hipStream_t s);

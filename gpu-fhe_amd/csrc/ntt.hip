@@ -954,20 +954,41 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   const u32 r = tr < skip_at ? tr : tr + skip_len;
   const u32 limb = __builtin_amdgcn_readfirstlane(r < n0 ? base0 + r : base1 + (r - n0));
   const ModParams m = mods[limb];
-  // the constants' 30-bit pieces (Sum30: four v_mad_u64_u32 per term, 2590 -> 2322 VALU per wave)
-  u64 h2[S];
-#pragma unroll
-  for (int k = 0; k < S; ++k) h2[k] = split30(hat[(u64)k * hs + limb].y);
   const u32 tp = Lay0::tpos(t);
   const gptr_u64 yb = (gptr_u64)(y + (u64)b * ybs + (u64)tile * G::SUBS_C + sub);
   u64 x[kE];
+  if constexpr (H == 16) {
+    // lz16 (every modulus < 2^60): plain sources, the S-term sum on 32-bit halves (dot_wide61:
+    // no splitting, the low column's carries from the mads) and the subtractive REDC into (0, 2q)
+    // (mont_redc: mont_redc_x's carry-mask asm does not survive this kernel's register allocation)
+    u64 hk[S];
 #pragma unroll
-  for (int j = 0; j < kE; ++j) {
-    const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
-    Sum30 acc;
+    for (int k = 0; k < S; ++k) hk[k] = hat[(u64)k * hs + limb].y;
+    const u64 qi = 0 - m.qinv;  // q^-1 mod 2^64
 #pragma unroll
-    for (int k = 0; k < S; ++k) acc.add(yb[yoff.o[k] + i], h2[k]);  // sources arrive pre-split
-    x[j] = acc.mont_lazy(m.q, m.qinv);  // [0, 2q): the pass takes inputs below 2q
+    for (int j = 0; j < kE; ++j) {
+      const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
+      u64 ys[S];
+#pragma unroll
+      for (int k = 0; k < S; ++k) ys[k] = yb[yoff.o[k] + i];
+      u64 tlo, thi;
+      dot_wide61<S>(ys, hk, tlo, thi);
+      x[j] = mont_redc(tlo, thi, m.q, qi);  // (0, 2q): the pass takes inputs below 2q
+    }
+  } else {
+    // the constants' 30-bit pieces (Sum30: four v_mad_u64_u32 per term; sources arrive pre-split,
+    // ks_split30)
+    u64 h2[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) h2[k] = split30(hat[(u64)k * hs + limb].y);
+#pragma unroll
+    for (int j = 0; j < kE; ++j) {
+      const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
+      Sum30 acc;
+#pragma unroll
+      for (int k = 0; k < S; ++k) acc.add(yb[yoff.o[k] + i], h2[k]);
+      x[j] = acc.mont_lazy(m.q, m.qinv);  // [0, 2q): the pass takes inputs below 2q
+    }
   }
   pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2>(
       x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,

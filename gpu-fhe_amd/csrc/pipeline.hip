@@ -98,7 +98,7 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   int rc;
   const bool prep = ks_prepared(c);  // the INTT emits ModUp's scaled inputs
   if ((rc = launch_ntt_strided(c, false, d + 2 * ln, 3 * ln, c_all, ln, batch, 0, L, s,
-                               prep ? c->d_nfold_up : nullptr, prep)))
+                               prep ? c->d_nfold_up : nullptr, prep && ks_split30(c))))
     return rc;
   // d2 (NTT form) as a contiguous [batch][L][N] operand: parked in the relinearised-ct buffer,
   // which is free until the combine

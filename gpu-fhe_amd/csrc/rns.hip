@@ -208,15 +208,16 @@ __global__ __launch_bounds__(kThreads) void k_modup_scale(const u64* __restrict_
                                                           u64* __restrict__ y, u32 S,
                                                           u32 log_n,
                                                           const ulonglong2* __restrict__ inv,
-                                                          const ModParams* __restrict__ mods) {
+                                                          const ModParams* __restrict__ mods,
+                                                          bool split) {
   const u64 n = 1ull << log_n;
   const u32 k = blockIdx.y, b = blockIdx.z;
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   const u64 q = mods[mod0 + k].q;
   const ulonglong2 w = inv[k];
-  // split30: k_modup_col reads its sources as Sum30 pieces
-  y[((u64)b * S + k) * n + i] =
-      split30(csub(shoup_lazy(in[(u64)b * in_bs + koff.o[k] + i], w.x, w.y, q), q));
+  // split30: k_modup_col reads its sources as Sum30 pieces on non-lz16 contexts (ks_split30)
+  const u64 v = csub(shoup_lazy(in[(u64)b * in_bs + koff.o[k] + i], w.x, w.y, q), q);
+  y[((u64)b * S + k) * n + i] = split ? split30(v) : v;
 }
 
 // host Shoup-pair table -> device ulonglong2 array (same 16-byte layout)
@@ -412,7 +413,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
       if (!call.scaled) {
         k_modup_scale<<<dim3((u32)(n / kThreads), S, batch), kThreads, 0, s>>>(
             call.ptr, call.bs, ko, lo, yws, S, c->log_n, c->d_modup_inv + (size_t)j * alpha,
-            c->d_mods);
+            c->d_mods, ks_split30(c));
         FHE_HIP_CHECK(hipGetLastError());
         ysrc = yws;
         ybs = (u64)S * n;
@@ -469,7 +470,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     // folds N^-1 (P^_k)^-1, c->d_nfold_down): no separate scaling pass
     u64* ydn = ext;
     if ((rc = launch_ntt_strided(c, false, accp, rn, ydn, (u64)K * n, 2 * batch, L, K, s,
-                                 c->d_nfold_down, true)))
+                                 c->d_nfold_down, ks_split30(c))))
       return rc;
     prof_mark(s, "ks_moddown_conv");
     const ModUpColArgs md{ydn, (u64)K * n, {0, n, 2 * n, 3 * n}, conv, (u64)nlimbs * n, K, nlimbs,
