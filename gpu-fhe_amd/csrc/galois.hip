@@ -112,24 +112,6 @@ __global__ __launch_bounds__(kThreads) void k_rescale_finish(u64* __restrict__ o
   out[(p * (nl - 1) + i) * n + c] = csub(shoup_lazy(d, w.x, w.y, q), q);
 }
 
-// Rotation combine: out[b][0] = (out[b][0] + ks0[b]) mod q, out[b][1] = ks1[b] (out[b][0] already
-// holds sigma_k(c0)).  Grid: x over coefficients, y = limb, z = ciphertext.
-__global__ __launch_bounds__(kThreads) void k_rotate_combine(u64* __restrict__ out,
-                                                             const u64* __restrict__ ks0,
-                                                             const u64* __restrict__ ks1, u32 L,
-                                                             u32 log_n,
-                                                             const ModParams* __restrict__ mods) {
-  const u64 n = 1ull << log_n;
-  const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 l = blockIdx.y;
-  const u64 b = blockIdx.z;
-  const u64 q = mods[l].q;
-  const u64 ln = (u64)L * n, e = b * ln + (u64)l * n + c;
-  u64* o = out + b * 2 * ln + (u64)l * n + c;
-  o[0] = csub(o[0] + ks0[e], q);
-  o[ln] = ks1[e];
-}
-
 inline u64 modinv_u64(u64 a, u64 q) { return powmod_u64(a % q, q - 2, q); }
 
 // k^-1 mod 2^bits for odd k (Newton: each step doubles the correct low bits)
@@ -210,6 +192,18 @@ int launch_rescale(const fhe_ctx* c, u64* out, const u64* in, u32 polys, u32 nl,
     return rc;
   k_rescale_spread<<<g, kThreads, 0, s>>>(tmp, last, nl, c->log_n, half, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
+  if (!c->wide) {
+    // the finish rides on the NTT's row-forward pass (k_moddown_row with one half and the
+    // q_last^-1 table): out_i = (x_i - NTT(tmp)_i) q_last^-1 straight from registers, no NTT-form
+    // tmp round trip and no separate finish pass
+    const u64 sn = (u64)(nl - 1) * n;
+    if ((rc = launch_ntt_col_fwd(c, tmp, sn, tmp, sn, polys, 0, nl - 1, s))) return rc;
+    ModDownRowArgs da{tmp, out, out, in, 0, nl, nl - 1, 0, polys, KsEpilogue{}};
+    da.ep.out_bs = sn;
+    da.halves = 1;
+    da.pinv = tab;
+    return launch_moddown_row(c, da, s);
+  }
   if ((rc = launch_ntt(c, true, tmp, tmp, polys, (u64)(nl - 1) * n, 0, nl - 1, s))) return rc;
   k_rescale_finish<<<g, kThreads, 0, s>>>(out, in, tmp, nl, c->log_n, tab, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
@@ -217,8 +211,8 @@ int launch_rescale(const fhe_ctx* c, u64* out, const u64* in, u32 polys, u32 nl,
 }
 
 size_t rotate_workspace_bytes(const fhe_ctx* c, u32 batch) {
-  // sigma(c1) [batch][L][N], ks0 and ks1 [batch][L][N], then the key-switch's own workspace
-  return 3 * (size_t)batch * c->L * c->n * sizeof(u64) + keyswitch_workspace_bytes(c, c->L, batch);
+  // sigma(c1) and sigma(c0) [batch][L][N], then the key-switch's own workspace
+  return 2 * (size_t)batch * c->L * c->n * sizeof(u64) + keyswitch_workspace_bytes(c, c->L, batch);
 }
 
 int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, const u64* rot_b,
@@ -231,11 +225,10 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
   const u32 L = c->L;
   const u64 n = c->n, ln = (u64)L * n;
   u64* sc1 = static_cast<u64*>(ws);  // [batch][L][N]
-  u64* ks0 = sc1 + batch * ln;
-  u64* ks1 = ks0 + batch * ln;
-  u64* kws = ks1 + batch * ln;
+  u64* sc0 = sc1 + batch * ln;
+  u64* kws = sc0 + batch * ln;
   int rc;
-  if ((rc = launch_automorphism(c, out, 2 * ln, in, 2 * ln, batch, 0, L, galois_elt, true, s)) ||
+  if ((rc = launch_automorphism(c, sc0, ln, in, 2 * ln, batch, 0, L, galois_elt, true, s)) ||
       (rc = launch_automorphism(c, sc1, ln, in + ln, 2 * ln, batch, 0, L, galois_elt, true, s)))
     return rc;
   // key-switch sigma(c1): its coefficient form goes to the tail of the key-switch workspace
@@ -247,12 +240,13 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
     return rc;
   CAll call = CAll::contiguous(c_all, L, n);
   call.scaled = prep;
-  if ((rc = launch_keyswitch_shard(c, ks0, ks1, call, sc1, rot_b, rot_a, 0, L, batch, kws, s)))
-    return rc;
-  k_rotate_combine<<<dim3((u32)(n / kThreads), L, batch), kThreads, 0, s>>>(out, ks0, ks1, L,
-                                                                           c->log_n, c->d_mods);
-  FHE_HIP_CHECK(hipGetLastError());
-  return kOk;
+  // out = (sigma(c0) + ks0, ks1) straight out of the key-switch's ModDown finish (KsEpilogue)
+  KsEpilogue ep;
+  ep.out_bs = 2 * ln;
+  ep.add0 = sc0;
+  ep.add_bs = ln;
+  return launch_keyswitch_shard(c, out, out + ln, call, sc1, rot_b, rot_a, 0, L, batch, kws, s,
+                                &ep);
 }
 
 }  // namespace fhe

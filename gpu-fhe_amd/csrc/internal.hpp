@@ -124,6 +124,17 @@ struct ModUpColArgs {
 int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s);
 // ModDown finish fused into the conversion NTT's row-forward pass (ntt.hip, k_moddown_row): conv
 // [2][batch][nq][N] column-passed -> ks{0,1} [batch][nq][N] = (acc - NTT(conv)) P^-1 mod q.
+// Optional epilogue of a key-switch's ModDown finish: the outputs of ciphertext b land at
+// ks{0,1} + b * out_bs (rows of N words), and with add{0,1} set the finish writes
+// add_h[b * add_bs + row N + i] + ks_h mod q instead of ks_h -- the relinearisation / rotation
+// combine folded into the last pass (no separate read of ks0 / ks1).  Defaults: contiguous
+// [batch][nlimbs][N] outputs, nothing added.
+struct KsEpilogue {
+  u64 out_bs = 0;  // 0: nlimbs * N
+  const u64* add0 = nullptr;
+  const u64* add1 = nullptr;
+  u64 add_bs = 0;
+};
 struct ModDownRowArgs {
   const u64* conv;
   u64* ks0;
@@ -131,6 +142,11 @@ struct ModDownRowArgs {
   const u64* acc;
   u64 acc_ws;
   u32 rows, nq, limb0, batch;
+  KsEpilogue ep;  // out_bs resolved (non-zero)
+  // 2: the key-switch's two accumulators (h = 0 -> ks0, 1 -> ks1; conv [2][batch][nq][N]);
+  // 1: one set of polys (ks0 only, conv [batch][nq][N]), as the NTT-form rescale uses it
+  u32 halves = 2;
+  const ulonglong2* pinv = nullptr;  // per-limb Shoup pairs of the divisor's inverse; null: P^-1
 };
 int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s);
 // Fused ct x ct tensor: a, b [batch][2][nlimbs][N] coefficient form -> d [batch][3][nlimbs][N].
@@ -189,7 +205,8 @@ inline bool ks_prepared(const fhe_ctx* c) {
 inline bool ks_split30(const fhe_ctx* c) { return !c->lz16; }
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
-                           u32 nlimbs, u32 batch, void* ws, hipStream_t s);
+                           u32 nlimbs, u32 batch, void* ws, hipStream_t s,
+                           const KsEpilogue* ep = nullptr);
 size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch);
 // Fast basis extension between contiguous ctx limb ranges: in [S][N] over limbs [s0, s0+S),
 // out [T][N] over limbs [t0, t0+T) (ranges disjoint).

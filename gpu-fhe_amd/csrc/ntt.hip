@@ -1003,9 +1003,15 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
 struct FinishView {
   u64* out;
   const u64* acc;
+  const u64* add;  // the KsEpilogue's addend rows, or null
   u32 lane;
   u64 q;
   ulonglong2 pinv;
+  __device__ __forceinline__ u64x2_t plus(u64x2_t r, u32 off) const {
+    if (!add) return r;  // kernel-argument uniform
+    const u64x2_t a = *(const __attribute__((address_space(1))) u64x2_t*)(add + off);
+    return u64x2_t{csub(r.x + a.x, q), csub(r.y + a.y, q)};
+  }
   template <class Lay>
   __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
     static_assert(contiguous16<Lay>(), "the last forward row round is contiguous");
@@ -1017,7 +1023,7 @@ struct FinishView {
       const u64x2_t av = a[j];
       const u64 r0 = csub(shoup_lazy(av.x + q - x[2 * j], pinv.x, pinv.y, q), q);
       const u64 r1 = csub(shoup_lazy(av.y + q - x[2 * j + 1], pinv.x, pinv.y, q), q);
-      o[j] = u64x2_t{r0, r1};
+      o[j] = plus(u64x2_t{r0, r1}, off + 2 * j);
     }
   }
   template <u32 TPS>
@@ -1029,7 +1035,7 @@ struct FinishView {
       const u64x2_t av = a[jj * TPS];
       const u64 r0 = csub(shoup_lazy(av.x + q - x[2 * jj], pinv.x, pinv.y, q), q);
       const u64 r1 = csub(shoup_lazy(av.y + q - x[2 * jj + 1], pinv.x, pinv.y, q), q);
-      o[jj * TPS] = u64x2_t{r0, r1};
+      o[jj * TPS] = plus(u64x2_t{r0, r1}, lane + 2 * (t + jj * TPS));
     }
   }
 };
@@ -1038,9 +1044,10 @@ template <int LOGN, int H>
 __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __restrict__ ks0,
                                         u64* __restrict__ ks1, const u64* __restrict__ acc,
                                         u64 acc_ws, u32 rows, u32 nq, u32 limb0, u32 batch,
-                                        u32 items, const ulonglong2* __restrict__ pinv,
+                                        u32 items, u32 halves,
+                                        const ulonglong2* __restrict__ pinv,
                                         const ulonglong2* __restrict__ tw_all,
-                                        const ModParams* __restrict__ mods) {
+                                        const ModParams* __restrict__ mods, KsEpilogue ep) {
   using G = Geo<LOGN>;
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[G::LDS_R];
@@ -1048,7 +1055,7 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   const LView<1, true> lv{lds + sub * G::RS};
   const u32 it = blockIdx.x;
   if (it >= items) return;
-  const u32 polys = 2 * batch;
+  const u32 polys = halves * batch;
   u32 l, rest;
   xcd_limb_split(it, nq, items / nq, l, rest);
   const u32 p = rest % polys, tile = rest / polys;
@@ -1061,8 +1068,10 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   u64 x[kE];
   pass_load<G::N2, true>(GView<1>{const_cast<u64*>(conv) + ((u64)p * nq + l) * N + rloc, lane}, t,
                          x);
-  const FinishView fo{(h ? ks1 : ks0) + ((u64)b * nq + l) * N + rloc,
-                      acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc, lane, q,
+  const u64* add = h ? ep.add1 : ep.add0;
+  const FinishView fo{(h ? ks1 : ks0) + (u64)b * ep.out_bs + (u64)l * N + rloc,
+                      acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc,
+                      add ? add + (u64)b * ep.add_bs + (u64)l * N + rloc : nullptr, lane, q,
                       pinv[limb]};
   // column-passed by k_modup_col (inputs below 2q) or k_ntt_col (below q)
   pass_run<G::N2, true, kFinalFwd, kWaveSync, true, H, fwd_range(2, G::N1, H), true>(
@@ -1450,10 +1459,10 @@ namespace {
 template <int LOGN, int HD>
 void moddown_row_dispatch(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s) {
   using G = Geo<LOGN>;
-  const u64 items = (u64)2 * a.batch * a.nq * G::TILES_R;
+  const u64 items = (u64)a.halves * a.batch * a.nq * G::TILES_R;
   k_moddown_row<LOGN, HD><<<dim3((u32)((items + 7) / 8 * 8)), G::THR_R, 0, s>>>(
-      a.conv, a.ks0, a.ks1, a.acc, a.acc_ws, a.rows, a.nq, a.limb0, a.batch, (u32)items,
-      c->d_pinv, c->d_tw_fwd, c->d_mods);
+      a.conv, a.ks0, a.ks1, a.acc, a.acc_ws, a.rows, a.nq, a.limb0, a.batch, (u32)items, a.halves,
+      a.pinv ? a.pinv : c->d_pinv, c->d_tw_fwd, c->d_mods, a.ep);
 }
 }  // namespace
 

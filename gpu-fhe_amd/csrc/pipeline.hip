@@ -2,7 +2,8 @@
 // the CKKS ct x ct product as it is used in practice, everything in NTT form:
 //   d = (a0 b0, a0 b1 + a1 b0, a1 b1)            elementwise tensor (k_tensor_ntt)
 //   (ks0, ks1) = KeySwitch(d2, relin key)          the batched hybrid key-switch (rns.hip)
-//   ct = (d0 + ks0, d1 + ks1)                      (k_relin_combine)
+//   ct = (d0 + ks0, d1 + ks1)                      folded into the key-switch's ModDown finish
+//                                                  (KsEpilogue: no separate combine pass)
 //   [optional] ct = Rescale(ct)                    divide-and-round by the last modulus (galois.hip)
 // Restated by oracle/pyoracle.py (mul_relin); not in the reference, whose only ciphertext
 // operation is poly_add (/root/reference/ polynomial.py:3-5).  The launches never allocate or
@@ -16,9 +17,11 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// a, b [batch][2][L][N] NTT form, canonical -> d [batch][3][L][N] canonical.  Grid: x over
-// coefficients, y = limb, z = ciphertext.
+// a, b [batch][2][L][N] NTT form, canonical -> d0, d1 into d [batch][2][L][N] and d2 into its own
+// contiguous [batch][L][N] (the key-switch's operand, no gather copy).  Grid: x over coefficients,
+// y = limb, z = ciphertext.
 __global__ __launch_bounds__(kThreads) void k_tensor_ntt(u64* __restrict__ d,
+                                                         u64* __restrict__ d2,
                                                          const u64* __restrict__ a,
                                                          const u64* __restrict__ b, u32 L,
                                                          u32 log_n,
@@ -32,38 +35,20 @@ __global__ __launch_bounds__(kThreads) void k_tensor_ntt(u64* __restrict__ d,
   const u64 a0 = a[off], a1 = a[off + ln], b0 = b[off], b1 = b[off + ln];
   const u128 t0 = (u128)a0 * b0, t2 = (u128)a1 * b1;
   const u128 t1 = (u128)a0 * b1 + (u128)a1 * b0;
-  u64* o = d + bt * 3 * ln + (u64)l * n + c;
+  u64* o = d + bt * 2 * ln + (u64)l * n + c;
   o[0] = reduce128_any((u64)t0, (u64)(t0 >> 64), m);
   o[ln] = reduce128_any((u64)t1, (u64)(t1 >> 64), m);
-  o[2 * ln] = reduce128_any((u64)t2, (u64)(t2 >> 64), m);
-}
-
-// out[b][0] = d[b][0] + ks0[b], out[b][1] = d[b][1] + ks1[b] (mod q).
-__global__ __launch_bounds__(kThreads) void k_relin_combine(u64* __restrict__ out,
-                                                            const u64* __restrict__ d,
-                                                            const u64* __restrict__ ks0,
-                                                            const u64* __restrict__ ks1, u32 L,
-                                                            u32 log_n,
-                                                            const ModParams* __restrict__ mods) {
-  const u64 n = 1ull << log_n, ln = (u64)L * n;
-  const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 l = blockIdx.y;
-  const u64 bt = blockIdx.z;
-  const u64 q = mods[l].q;
-  const u64 e = bt * ln + (u64)l * n + c;
-  const u64* di = d + bt * 3 * ln + (u64)l * n + c;
-  u64* o = out + bt * 2 * ln + (u64)l * n + c;
-  o[0] = csub(di[0] + ks0[e], q);
-  o[ln] = csub(di[ln] + ks1[e], q);
+  d2[bt * ln + (u64)l * n + c] = reduce128_any((u64)t2, (u64)(t2 >> 64), m);
 }
 
 }  // namespace
 
 size_t mul_relin_workspace_bytes(const fhe_ctx* c, u32 batch) {
   const size_t ln = (size_t)c->L * c->n * sizeof(u64);
-  // d [3], ks0 + ks1 [2], relinearised ct before the rescale [2], the rescale's own [2 L N]
-  // workspace, the key-switch's workspace (its tail holds INTT(d2))
-  return (size_t)batch * ln * (3 + 2 + 2) + rescale_workspace_bytes(c, 2 * batch, c->L) +
+  // d0, d1 [2], relinearised ct before the rescale [2] (d2 parks there until the key-switch's
+  // finish), the rescale's own [2 L N] workspace, the key-switch's workspace (its tail holds
+  // INTT(d2))
+  return (size_t)batch * ln * (2 + 2) + rescale_workspace_bytes(c, 2 * batch, c->L) +
          keyswitch_workspace_bytes(c, c->L, batch);
 }
 
@@ -80,15 +65,16 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   if (batch == 0) return kOk;
   const u32 L = c->L;
   const u64 n = c->n, ln = (u64)L * n;
-  u64* d = static_cast<u64*>(ws);        // [batch][3][L][N]
-  u64* ks0 = d + 3 * batch * ln;         // [batch][L][N]
-  u64* ks1 = ks0 + batch * ln;
-  u64* rl = ks1 + batch * ln;            // [batch][2][L][N] relinearised, before the rescale
+  u64* d = static_cast<u64*>(ws);        // [batch][2][L][N]: d0, d1
+  u64* rl = d + 2 * batch * ln;          // [batch][2][L][N] relinearised, before the rescale
   u64* rws = rl + 2 * batch * ln;        // rescale workspace
   u64* kws = reinterpret_cast<u64*>(reinterpret_cast<char*>(rws) +
                                     rescale_workspace_bytes(c, 2 * batch, L));
   const dim3 g((u32)(n / kThreads), L, batch);
-  k_tensor_ntt<<<g, kThreads, 0, s>>>(d, a, b, L, c->log_n, c->d_mods);
+  // d2 (NTT form) as a contiguous [batch][L][N] operand for the key-switch: parked in the
+  // relinearised-ct buffer, which is free until the combine
+  u64* d2 = rl;
+  k_tensor_ntt<<<g, kThreads, 0, s>>>(d, d2, a, b, L, c->log_n, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
   prof_mark(s, "tensor_ntt");
   // d2 = d[b][2]: gather to a contiguous [batch][L][N] operand for the key-switch (its INTT lands
@@ -97,21 +83,23 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   u64* c_all = reinterpret_cast<u64*>(reinterpret_cast<char*>(kws) + kbytes) - batch * ln;
   int rc;
   const bool prep = ks_prepared(c);  // the INTT emits ModUp's scaled inputs
-  if ((rc = launch_ntt_strided(c, false, d + 2 * ln, 3 * ln, c_all, ln, batch, 0, L, s,
+  if ((rc = launch_ntt_strided(c, false, d2, ln, c_all, ln, batch, 0, L, s,
                                prep ? c->d_nfold_up : nullptr, prep && ks_split30(c))))
     return rc;
-  // d2 (NTT form) as a contiguous [batch][L][N] operand: parked in the relinearised-ct buffer,
-  // which is free until the combine
-  u64* d2 = rl;
-  FHE_HIP_CHECK(hipMemcpy2DAsync(d2, ln * sizeof(u64), d + 2 * ln, 3 * ln * sizeof(u64),
-                                 ln * sizeof(u64), batch, hipMemcpyDeviceToDevice, s));
   CAll call = CAll::contiguous(c_all, L, n);
   call.scaled = prep;
-  if ((rc = launch_keyswitch_shard(c, ks0, ks1, call, d2, evk_b, evk_a, 0, L, batch, kws, s)))
-    return rc;
+  // the relinearised ciphertext (d0 + ks0, d1 + ks1) straight out of the ModDown finish
+  // ([batch][2][L][N] outputs and addends, 2 L N apart per ciphertext); d2's slot in rl is dead
+  // by then (read by the INTT and the inner product only)
   u64* dst = rescale ? rl : out;
-  k_relin_combine<<<g, kThreads, 0, s>>>(dst, d, ks0, ks1, L, c->log_n, c->d_mods);
-  FHE_HIP_CHECK(hipGetLastError());
+  KsEpilogue ep;
+  ep.out_bs = 2 * ln;
+  ep.add0 = d;
+  ep.add1 = d + ln;
+  ep.add_bs = 2 * ln;
+  if ((rc = launch_keyswitch_shard(c, dst, dst + ln, call, d2, evk_b, evk_a, 0, L, batch, kws, s,
+                                   &ep)))
+    return rc;
   prof_mark(s, "relin_combine");
   if (rescale) {
     if ((rc = launch_rescale(c, out, rl, 2 * batch, L, true, rws, s))) return rc;

@@ -178,6 +178,7 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc, u6
 
 // out{0,1}[b][r][i] = (acc{0,1}[b][r][i] - conv{0,1}[b][r][i]) * P^-1 mod q over own Q-limbs.
 // Grid: x over coefficients, y = own Q-limb r, z = batch entry b.
+// (with the KsEpilogue: outputs at b * out_bs, plus add{0,1} when set)
 __global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ out0,
                                                              u64* __restrict__ out1,
                                                              const u64* __restrict__ acc,
@@ -185,7 +186,8 @@ __global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ o
                                                              const u64* __restrict__ conv,
                                                              u32 nq, u32 limb0, u32 log_n,
                                                              const ulonglong2* __restrict__ pinv,
-                                                             const ModParams* __restrict__ mods) {
+                                                             const ModParams* __restrict__ mods,
+                                                             KsEpilogue ep) {
   const u64 n = 1ull << log_n;
   const u32 r = blockIdx.y, b = blockIdx.z;
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -196,8 +198,14 @@ __global__ __launch_bounds__(kThreads) void k_moddown_finish(u64* __restrict__ o
   const u64 e = ((u64)b * nq + r) * n + i;
   const u64 ai = ((u64)b * rows + r) * n + i;  // acc rows [0, nq) are the own Q-limbs
   const u64 c0 = conv[e], c1 = conv[total + e];
-  out0[e] = csub(shoup_lazy(acc[ai] + q - c0, w.x, w.y, q), q);
-  out1[e] = csub(shoup_lazy(acc[acc_ws + ai] + q - c1, w.x, w.y, q), q);
+  u64 r0 = csub(shoup_lazy(acc[ai] + q - c0, w.x, w.y, q), q);
+  u64 r1 = csub(shoup_lazy(acc[acc_ws + ai] + q - c1, w.x, w.y, q), q);
+  const u64 ea = (u64)b * ep.add_bs + (u64)r * n + i;
+  if (ep.add0) r0 = csub(r0 + ep.add0[ea], q);
+  if (ep.add1) r1 = csub(r1 + ep.add1[ea], q);
+  const u64 eo = (u64)b * ep.out_bs + (u64)r * n + i;
+  out0[eo] = r0;
+  out1[eo] = r1;
 }
 
 // Prologue of the fused conversion column pass (ntt.hip k_modup_col), ModUp and ModDown:
@@ -360,7 +368,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
 
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
-                           u32 nlimbs, u32 batch, void* ws, hipStream_t s) {
+                           u32 nlimbs, u32 batch, void* ws, hipStream_t s,
+                           const KsEpilogue* epi) {
   if (c->K == 0) {
     set_error("keyswitch: context has no special primes (K = 0)");
     return kInvalid;
@@ -370,6 +379,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     return kUnsupported;
   }
   if (batch == 0) return kOk;
+  KsEpilogue ep = epi ? *epi : KsEpilogue{};
+  if (ep.out_bs == 0) ep.out_bs = (u64)nlimbs * c->n;
   const u32 L = c->L, K = c->K, M = L + K, alpha = c->alpha, rows = nlimbs + K;
   const u64 n = c->n, rn = (u64)rows * n, B = batch;
   u64* ext = static_cast<u64*>(ws);          // [dnum][B][rows][N]
@@ -477,7 +488,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
                           nlimbs, 0, nlimbs, limb0, 0, 2 * batch, c->d_moddown_hat, M};
     if ((rc = launch_modup_col(c, md, s))) return rc;
     prof_mark(s, "ks_moddown_col");
-    const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch};
+    const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch, ep};
     if ((rc = launch_moddown_row(c, da, s))) return rc;
     prof_mark(s, "moddown_row_finish");
     return kOk;
@@ -493,7 +504,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
                                  nlimbs, s)))
       return rc;
     prof_mark(s, "ks_moddown_col");
-    const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch};
+    const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch, ep};
     if ((rc = launch_moddown_row(c, da, s))) return rc;
     prof_mark(s, "moddown_row_finish");
     return kOk;
@@ -501,7 +512,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   if ((rc = launch_ntt(c, true, conv, conv, 2 * batch, (u64)nlimbs * n, limb0, nlimbs, s)))
     return rc;
   k_moddown_finish<<<dim3((u32)(n / kThreads), nlimbs, batch), kThreads, 0, s>>>(
-      ks0, ks1, acc, acc_ws, rows, conv, nlimbs, limb0, c->log_n, c->d_pinv, c->d_mods);
+      ks0, ks1, acc, acc_ws, rows, conv, nlimbs, limb0, c->log_n, c->d_pinv, c->d_mods, ep);
   FHE_HIP_CHECK(hipGetLastError());
   prof_mark(s, "moddown_finish");
   return kOk;
