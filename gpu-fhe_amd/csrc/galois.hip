@@ -19,15 +19,6 @@ constexpr int kThreads = 256;
 
 __device__ __forceinline__ u32 brv(u32 x, u32 bits) { return __builtin_bitreverse32(x) >> (32 - bits); }
 
-// t < 2^64 -> t mod q (Shoup by 1: [0, 3q), then two subtractions; wide moduli 2^61 <= q < 2^63:
-// the exact quotient, [0, 2q), one subtraction)
-__device__ __forceinline__ u64 reduce_word(u64 t, const ModParams& m) {
-  if (m.mu == 0) return csub(shoup_lazy(t, 1, m.ones, m.q), m.q);
-  u64 r = shoup_q3(t, 1, m.ones, 0 - m.q);
-  r = csub(r, 2 * m.q);
-  return csub(r, m.q);
-}
-
 // Grid: x over coefficients, y = limb, z = poly.  in/out rows at stride N, polys at pin / pout.
 __global__ __launch_bounds__(kThreads) void k_automorph(u64* __restrict__ out, u64 pout,
                                                         const u64* __restrict__ in, u64 pin,
@@ -190,20 +181,20 @@ int launch_rescale(const fhe_ctx* c, u64* out, const u64* in, u32 polys, u32 nl,
   if ((rc = launch_ntt_strided(c, false, in + (u64)(nl - 1) * n, (u64)nl * n, last, n, polys,
                                 nl - 1, 1, s)))
     return rc;
-  k_rescale_spread<<<g, kThreads, 0, s>>>(tmp, last, nl, c->log_n, half, c->d_mods);
-  FHE_HIP_CHECK(hipGetLastError());
   if (!c->wide) {
-    // the finish rides on the NTT's row-forward pass (k_moddown_row with one half and the
-    // q_last^-1 table): out_i = (x_i - NTT(tmp)_i) q_last^-1 straight from registers, no NTT-form
-    // tmp round trip and no separate finish pass
+    // the spread rides on the column-forward pass (k_rescale_col) and the finish on the row-forward
+    // pass (k_moddown_row with one half and the q_last^-1 table): out_i = (x_i - NTT(tmp)_i)
+    // q_last^-1 straight from registers; tmp exists only column-passed
     const u64 sn = (u64)(nl - 1) * n;
-    if ((rc = launch_ntt_col_fwd(c, tmp, sn, tmp, sn, polys, 0, nl - 1, s))) return rc;
+    if ((rc = launch_rescale_col(c, last, tmp, polys, nl - 1, half, s))) return rc;
     ModDownRowArgs da{tmp, out, out, in, 0, nl, nl - 1, 0, polys, KsEpilogue{}};
     da.ep.out_bs = sn;
     da.halves = 1;
     da.pinv = tab;
     return launch_moddown_row(c, da, s);
   }
+  k_rescale_spread<<<g, kThreads, 0, s>>>(tmp, last, nl, c->log_n, half, c->d_mods);
+  FHE_HIP_CHECK(hipGetLastError());
   if ((rc = launch_ntt(c, true, tmp, tmp, polys, (u64)(nl - 1) * n, 0, nl - 1, s))) return rc;
   k_rescale_finish<<<g, kThreads, 0, s>>>(out, in, tmp, nl, c->log_n, tab, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());

@@ -149,6 +149,10 @@ struct ModDownRowArgs {
   const ulonglong2* pinv = nullptr;  // per-limb Shoup pairs of the divisor's inverse; null: P^-1
 };
 int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s);
+// NTT-form rescale, spread + column-forward pass in one (ntt.hip, k_rescale_col): last [polys][N]
+// (coefficient form of limb nq) -> dst [polys][nq][N] column-passed; half = rescale half table.
+int launch_rescale_col(const fhe_ctx* c, const u64* last, u64* dst, u32 polys, u32 nq,
+                       const u64* half, hipStream_t s);
 // Fused ct x ct tensor: a, b [batch][2][nlimbs][N] coefficient form -> d [batch][3][nlimbs][N].
 int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 batch, u32 limb0,
                    u32 nlimbs, void* ws, hipStream_t s);

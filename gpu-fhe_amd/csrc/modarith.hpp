@@ -370,6 +370,15 @@ __device__ __forceinline__ u64 reduce_u64(u64 x, const ModParams& m) {
   return barrett_reduce((u128)x, m);
 }
 
+// t < 2^64 -> t mod q (Shoup by 1: [0, 3q), then two subtractions; wide moduli 2^61 <= q < 2^63:
+// the exact quotient, [0, 2q), one subtraction)
+__device__ __forceinline__ u64 reduce_word(u64 t, const ModParams& m) {
+  if (m.mu == 0) return csub(shoup_lazy(t, 1, m.ones, m.q), m.q);
+  u64 r = shoup_q3(t, 1, m.ones, 0 - m.q);
+  r = csub(r, 2 * m.q);
+  return csub(r, m.q);
+}
+
 // Exact a * b mod q for a, b < q and any q < 2^64 (generic entry points only; the context
 // kernels use Shoup/Barrett).  q < 2^63: Barrett / reduce128_wide; above, a 64-step
 // double-and-add.

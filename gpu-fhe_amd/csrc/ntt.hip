@@ -1348,6 +1348,54 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;
 }
+// Rescale (NTT form): the spread of the last limb over the other limbs folded into the
+// column-forward pass.  last [polys][N] holds INTT(x_last); the tile of limb l (l < nq, the last
+// limb is nq) loads last's columns and spreads them in registers,
+//   v = ((last + h) mod q_last - h) mod q_l,  h = q_last / 2,   (galois.hip k_rescale_spread)
+// before the column-forward stages, writing dst [polys][nq][N]: no spread pass and no re-read of
+// its output.  The row pass is k_moddown_row with the q_last^-1 table (the finish).
+template <int LOGN, int H>
+__global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void
+k_rescale_col(const u64* __restrict__ last, u64* __restrict__ dst, u32 nq, u32 items,
+              const u64* __restrict__ half, const ulonglong2* __restrict__ tw_all,
+              const ModParams* __restrict__ mods) {
+  using G = Geo<LOGN>;
+  constexpr u64 N = 1ull << LOGN;
+  __shared__ u64 lds[G::LDS_C];
+  const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
+  const LViewC<G::SUBS_C> lv{lds + sub};
+  const u32 it = blockIdx.x;
+  if (it >= items) return;
+  u32 tile, pl;  // XCD-grouped placement as in k_ntt_col
+  if ((items / G::TILES_C) % 8 == 0) {
+    const u32 k = it / 8;
+    tile = k % G::TILES_C;
+    pl = (k / G::TILES_C) * 8 + it % 8;
+  } else {
+    tile = it % G::TILES_C;
+    pl = it / G::TILES_C;
+  }
+  const u32 l = __builtin_amdgcn_readfirstlane(pl % nq), p = pl / nq;
+  const u64 col = (u64)tile * G::SUBS_C;
+  u64 x[kE];
+  pass_load<G::N1, true>(GView<G::R2>{const_cast<u64*>(last) + (u64)p * N + col, sub}, t, x);
+  const ModParams ml = mods[nq], mi = mods[l];
+  const u64 h = ml.q >> 1, mh = mi.q - half[l];
+#pragma unroll
+  for (int j = 0; j < kE; ++j) x[j] = csub(reduce_word(csub(x[j] + h, ml.q), mi) + mh, mi.q);
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 1>(
+      x, GView<G::R2>{dst + (u64)pl * N + col, sub}, lv, t, tw_all + (u64)l * N, 1u, mi.q,
+      {0, 0}, {0, 0});
+}
+
+template <int LOGN, int HD>
+void rescale_col_dispatch(const fhe_ctx* c, const u64* last, u64* dst, u32 polys, u32 nq,
+                          const u64* half, hipStream_t s) {
+  using G = Geo<LOGN>;
+  const u64 ic = (u64)polys * nq * G::TILES_C;
+  k_rescale_col<LOGN, HD><<<item_grid(ic), G::THR_C, 0, s>>>(last, dst, nq, (u32)ic, half,
+                                                            c->d_tw_fwd, c->d_mods);
+}
 #endif  // !FHE_NTT_KS_ONLY
 
 }  // namespace
@@ -1552,6 +1600,29 @@ int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 bat
                    u32 nlimbs, void* ws, hipStream_t s) {
   if ((u64)batch * nlimbs == 0) return kOk;
   return hommult_chunk(c, d, a, b, batch, limb0, nlimbs, static_cast<u64*>(ws), s);
+}
+
+int launch_rescale_col(const fhe_ctx* c, const u64* last, u64* dst, u32 polys, u32 nq,
+                       const u64* half, hipStream_t s) {
+  if ((u64)polys * nq == 0) return kOk;
+  if (c->wide) {
+    set_error("rescale_col: the fused rescale needs every modulus < 2^61");
+    return kUnsupported;
+  }
+  switch (c->log_n) {
+#define X(n)                                                  \
+  case n:                                                     \
+    if (c->lz16)                                              \
+      rescale_col_dispatch<n, 16>(c, last, dst, polys, nq, half, s); \
+    else                                                      \
+      rescale_col_dispatch<n, 8>(c, last, dst, polys, nq, half, s);  \
+    FHE_HIP_CHECK(hipGetLastError());                         \
+    return kOk;
+    FHE_LOGN_CASES(X)
+#undef X
+  }
+  set_error("unsupported log_n");
+  return kUnsupported;
 }
 
 #endif  // FHE_NTT_KS_ONLY
