@@ -1351,7 +1351,8 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
 // Rescale (NTT form): the spread of the last limb over the other limbs folded into the
 // column-forward pass.  last [polys][N] holds INTT(x_last); the tile of limb l (l < nq, the last
 // limb is nq) loads last's columns and spreads them in registers,
-//   v = ((last + h) mod q_last - h) mod q_l,  h = q_last / 2,   (galois.hip k_rescale_spread)
+//   v = ((last + h) mod q_last - h) mod q_l,  h = q_last / 2   (galois.hip k_rescale_spread, the
+// path of wide contexts)
 // before the column-forward stages, writing dst [polys][nq][N]: no spread pass and no re-read of
 // its output.  The row pass is k_moddown_row with the q_last^-1 table (the finish).
 template <int LOGN, int H>

@@ -100,7 +100,7 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   if ((rc = launch_keyswitch_shard(c, dst, dst + ln, call, d2, evk_b, evk_a, 0, L, batch, kws, s,
                                    &ep)))
     return rc;
-  prof_mark(s, "relin_combine");
+  prof_mark(s, "relin_keyswitch");
   if (rescale) {
     if ((rc = launch_rescale(c, out, rl, 2 * batch, L, true, rws, s))) return rc;
     prof_mark(s, "rescale");
