@@ -247,6 +247,19 @@ constexpr int fwd_range(int r0, int stages, int H) {
   return r;
 }
 
+// Inverse lazy ranges for H = 16 (every q < 2^60, so values up to 16q fit), in units of q: the
+// range of element j before local stage k of a GS round whose inputs are below 3q.  Both elements of
+// a pair (j, j | 1 << b) share it (ranges depend only on the bits already processed).  The
+// difference leaves below 3q (Shoup); the sum leaves unreduced, below 2r q, except that a pair at
+// r = 12 is first reduced to 6 (2r <= 12 < 16).  Per 16-element round: 8 conditional subtractions
+// in the stages + 12 at the end (back below 3q for the exchange) instead of 32.
+constexpr int gs_red(int r) { return r > 8 ? 6 : r; }
+constexpr int gs_in(int j, int k) {
+  int r = 3;
+  for (int b = 0; b < k; ++b) r = ((j >> b) & 1) ? 3 : 2 * gs_red(r);
+  return r;
+}
+
 // Runs one round's butterfly stages on the 16 values a thread holds in registers.
 // Element j sits at sub-transform position tp | Lay::jpos(j).  `base` selects the twiddle rows:
 // local stage st, group g reads tw[(base << st) + g] (base = 1 for the column pass, R1 + row for
@@ -389,6 +402,52 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         }
       }
     });
+  } else if constexpr (H == 16) {
+    // GS with lazy sums (gs_in): inputs in [0, 3q); each pair at r q: sum u + v below 2r q,
+    // (u - v + r q) w -> [0, 3q); the round ends with every element back in [0, 3q)
+    u64 q6 = 6 * q;
+    asm("" : "+s"(q6));
+    constexpr bool kLast = FIN == kFinalInv || FIN == kFinalInvS30;
+    static_for<0, KB>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      constexpr int bitpos = LO + b;
+      constexpr int st = LOGR - 1 - bitpos;
+      static_for<0, E>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (!(j & (1 << b))) {
+          constexpr int jj = j | (1 << b);
+          constexpr int r = gs_in(j, b), rr = gs_red(r);
+          u64 u = x[j], v = x[jj];
+          if constexpr (rr != r) {
+            u = csubk(u, q6);
+            v = csubk(v, q6);
+          }
+          const u64 sum = u + v, dif = u - v + (rr == 3 ? q3 : q6);
+          if constexpr (kLast && st == 0) {
+            // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
+            x[j] = csubk(csubk(shoup_q3<GATHER>(sum, nf0.x, nf0.y, nq), q2), q);
+            x[jj] = csubk(csubk(shoup_q3<GATHER>(dif, nf1.x, nf1.y, nq), q2), q);
+          } else {
+            const ulonglong2 w = twiddle(b, j, bitpos, st);
+            x[j] = sum;
+            x[jj] = shoup_q3<GATHER>(dif, w.x, w.y, nq);
+          }
+        }
+      });
+    });
+    if constexpr (kLast) {
+      if constexpr (FIN == kFinalInvS30) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) x[j] = split30(x[j]);
+      }
+    } else {
+      static_for<0, E>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int r = gs_in(j, KB);
+        if constexpr (r > 6) x[j] = csubk(x[j], q6);
+        if constexpr (r > 3) x[j] = csubk(x[j], q3);
+      });
+    }
   } else {
     // GS: inputs in [0, 3q); sum -> [0, 3q); (u - v + 3q) w -> [0, 3q)
     static_for<0, KB>([&](auto bc) {
@@ -1251,7 +1310,7 @@ inline dim3 item_grid(u64 items) { return dim3((u32)((items + 7) / 8 * 8)); }
 
 // The inverse passes' H: the lazy inverse does not depend on the forward headroom (one build for
 // H = 8 and 16); wide contexts (H = 2) take the exact one.
-constexpr int inv_h(int hd) { return hd == 2 ? 2 : 8; }
+constexpr int inv_h(int hd) { return hd; }
 
 // Row pass of a standalone NTT over [polys][nlimbs][N] (src poly stride sp -> dst stride dp).
 template <int LOGN, int HD>

@@ -361,3 +361,56 @@ def test_keyswitch_inner_product_dot(q):
                   for _ in range(3000)]
         for xs, ks in cases:
             assert dot_wide61(xs, ks) == sum(x * k for x, k in zip(xs, ks))
+
+
+def gs_red(r):
+    return 6 if r > 8 else r
+
+
+def gs_in(j, k):
+    """ntt.hip gs_in: static range (units of q) of element j before local stage k of a round."""
+    r = 3
+    for b in range(k):
+        r = 3 if (j >> b) & 1 else 2 * gs_red(r)
+    return r
+
+
+@pytest.mark.parametrize("q", [m for m in _moduli() if m < 1 << 60])
+def test_lazy_gs_round(q):
+    """round_compute's H = 16 inverse (q < 2^60): a 16-element GS round with unreduced sums, the
+    pair reduction at r = 12 and the end-of-round subtractions.  Every value stays below its static
+    range (so below 12q < 2^64), the round leaves [0, 3q), and the outputs are congruent to the
+    exact GS butterflies' (sum, (u - v) w) on the same inputs and twiddles."""
+    rng = random.Random(q + 7)
+    q3, q6 = 3 * q, 6 * q
+    for trial in range(300):
+        # worst-case-heavy inputs below 3q
+        x = [rng.choice([0, q3 - 1, rng.randrange(q3)]) for _ in range(16)]
+        ref = [v % q for v in x]
+        tw = {(b, j): rng.randrange(q) for b in range(4) for j in range(16)}
+        for b in range(4):
+            for j in range(16):
+                if (j >> b) & 1:
+                    continue
+                jj = j | (1 << b)
+                r = gs_in(j, b)
+                assert gs_in(jj, b) == r
+                assert x[j] < r * q and x[jj] < r * q
+                u, v = x[j], x[jj]
+                rr = gs_red(r)
+                if rr != r:
+                    u, v = csub_fast(u, q6), csub_fast(v, q6)
+                    assert u < rr * q and v < rr * q
+                w = tw[(b, j)]
+                s, d = u + v, u - v + rr * q
+                assert s < 16 * q and 0 < d < 16 * q and s <= M64
+                x[j], x[jj] = s, shoup_q3(d, w, (w << 64) // q, q)
+                ref[j], ref[jj] = (ref[j] + ref[jj]) % q, (ref[j] - ref[jj]) * w % q
+        for j in range(16):
+            r = gs_in(j, 4)
+            assert x[j] < r * q
+            if r > 6:
+                x[j] = csub_fast(x[j], q6)
+            if r > 3:
+                x[j] = csub_fast(x[j], q3)
+            assert x[j] < q3 and x[j] % q == ref[j]
