@@ -6,13 +6,17 @@
 // register-resident data at full occupancy, with no memory traffic:
 //   forward  Cooley-Tukey, folded X-operand (shoup_q3_add), the 8q reduction every other stage
 //            (the row passes' schedule), outputs s and (2u + 3q) - s;
-//   inverse  Gentleman-Sande: sum mod 3q, (u - v + 3q) w by shoup_q3.
+//   inverse  Gentleman-Sande with lazy sums (round_compute's H = 16 form, gs_in ranges): sums
+//            unreduced, a pair at 12q reduced to 6q first, (u - v + r q) w by shoup_q3, and the
+//            round's end subtractions back below 3q.
 // Each thread holds kE = 16 values and runs 4-stage rounds on them exactly as a kernel round does
 // (8 butterflies per stage), with 8 twiddle pairs in registers standing in for the round's
 // gathered twiddles.  The result is the chip's butterflies/s ceiling for that arithmetic, measured
 // on the same box and clock regime as the kernels it is compared with.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "../../gpu-fhe_amd/csrc/modarith.hpp"
 
@@ -22,6 +26,22 @@ using fhe::u32;
 using fhe::u64;
 constexpr int kE = 16;
 constexpr int kThreads = 256;
+
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// ntt.hip gs_red / gs_in (the static per-element ranges of a lazy GS round)
+constexpr int gs_red(int r) { return r > 8 ? 6 : r; }
+constexpr int gs_in(int j, int k) {
+  int r = 3;
+  for (int b = 0; b < k; ++b) r = ((j >> b) & 1) ? 3 : 2 * gs_red(r);
+  return r;
+}
 
 __device__ __forceinline__ u64 csubk(u64 x, u64 m) {
   u64 nm = 0 - m;
@@ -41,9 +61,38 @@ __global__ __launch_bounds__(kThreads) void k_bfly_peak(u64* __restrict__ out,
 #pragma unroll
   for (int k = 0; k < 8; ++k) w[k] = tw[(gid + k) & 63];
   const u64 nq = 0 - q;
-  u64 q3 = 3 * q;
+  u64 q3 = 3 * q, q6 = 6 * q;
   asm("" : "+s"(q3));
+  asm("" : "+s"(q6));
   for (u32 r = 0; r < rounds; ++r) {
+    if constexpr (INV) {
+      static_for<0, 4>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        static_for<0, kE>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          if constexpr (!(j & (1 << b))) {
+            constexpr int jj = j | (1 << b);
+            constexpr int ri = gs_in(j, b), rr = gs_red(ri);
+            const ulonglong2 t = w[(j + b) & 7];
+            u64 u = x[j], v = x[jj];
+            if constexpr (rr != ri) {
+              u = csubk(u, q6);
+              v = csubk(v, q6);
+            }
+            const u64 sum = u + v, dif = u - v + (rr == 3 ? q3 : q6);
+            x[j] = sum;
+            x[jj] = fhe::shoup_q3<true>(dif, t.x, t.y, nq);
+          }
+        });
+      });
+      static_for<0, kE>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int ri = gs_in(j, 4);
+        if constexpr (ri > 6) x[j] = csubk(x[j], q6);
+        if constexpr (ri > 3) x[j] = csubk(x[j], q3);
+      });
+      continue;
+    }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
 #pragma unroll
@@ -60,11 +109,6 @@ __global__ __launch_bounds__(kThreads) void k_bfly_peak(u64* __restrict__ out,
           u64 t2 = (u << 1) + q3;
           FHE_OPAQUE(t2);
           x[jj] = t2 - s;
-        } else {
-          const u64 u = x[j], v = x[jj];
-          const u64 sum = u + v, dif = u - v + q3;
-          x[j] = csubk(sum, q3);
-          x[jj] = fhe::shoup_q3<true>(dif, t.x, t.y, nq);
         }
       }
     }
