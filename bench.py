@@ -298,7 +298,7 @@ def run_hommult(args, world, rank):
     if not args.bits > 60:  # the ceiling kernel runs the lazy (q < 2^61) arithmetic
         out["roofline_alu"] = roofline_alu(dom, 4 * rb * units, 3 * rb * units,
                                            kavg.get(dom, float("nan")),
-                                           {"forward": 17, "inverse": 18.6})  # row passes (mad-chain remainder; lazy GS round average)
+                                           {"forward": 16.25, "inverse": 18.2})  # lz16 row passes, round averages (bfly_peak.hip)
         full = (n // 2) * args.log_n
         out["hommult_pipeline_alu"] = roofline_alu("hm_col_fwd + hm_row_tensor + hm_col_inv",
                                                    4 * full * units, 3 * full * units,

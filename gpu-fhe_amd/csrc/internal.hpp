@@ -32,7 +32,9 @@ void prof_mark(hipStream_t s, const char* name);
 struct fhe_ctx {
   int device = 0;
   int num_cus = 0;  // compute units of `device` (one-generation grids of the item-loop kernels)
-  bool lz16 = false;  // every modulus < 2^60: forward NTTs may run lazy up to 16q (ntt.hip)
+  // every modulus < 2^60 and within 1/16 below a power of two: NTTs run lazy up to 16q with
+  // top-bits reductions (ntt.hip fwd_range, top_bits, gs_in)
+  bool lz16 = false;
   // some modulus in [2^61, 2^63): exact (non-lazy) butterflies, HD = 2 in ntt.hip, and the
   // unfused key-switch (rns.hip)
   bool wide = false;

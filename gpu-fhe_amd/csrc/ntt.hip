@@ -238,22 +238,33 @@ __device__ __forceinline__ u64 csubk(u64 x, u64 m) {
 
 // Forward lazy ranges, in units of q.  A CT stage maps X-operands below r q to
 // outputs below (r' + 3) q, where r' = r unless r + 3 would exceed the headroom H (values must stay
-// below H q <= 2^64), in which case X is first reduced by H/2 q (r' = H/2).  H = 16 needs q < 2^60
-// and subtracts at about every other stage; H = 8 (q < 2^61) at every stage once warm.
-constexpr int fwd_stage_out(int r, int H) { return (r + 3 > H ? H / 2 : r) + 3; }
+// below H q <= 2^64), in which case X is first reduced (r' = fwd_reduced(H)).  H = 8 (q < 2^61):
+// one subtraction of 4q, at every stage once warm.  H = 16 (lz16 contexts: every q < 2^60 and
+// within 1/16 below a power of two): the top-bits estimate x - (x >> s) q, s = bitlength(q), which
+// takes any x < 16q below 2q at the cost of one subtraction, so a reduction every fifth stage.
+constexpr int fwd_reduced(int H) { return H == 16 ? 2 : H / 2; }
+constexpr int fwd_stage_out(int r, int H) { return (r + 3 > H ? fwd_reduced(H) : r) + 3; }
+
+// x - floor(x / 2^s) q for x < 16 q, q in [2^s - 2^(s-4), 2^s): k = x >> s <= x / q and
+// x - k q < x (2^s - q) / 2^s + q < 2q (a shift, a v_mad_u64_u32, a v_mul_lo_u32 and an add; nq =
+// -q mod 2^64, the product exact mod 2^64 and the result >= 0)
+__device__ __forceinline__ u64 top_bits(u64 x, u32 s, u64 nq) {
+  return x + (u64)(u32)(x >> s) * nq;
+}
 constexpr int fwd_range(int r0, int stages, int H) {
   int r = r0;
   for (int i = 0; i < stages; ++i) r = fwd_stage_out(r, H);
   return r;
 }
 
-// Inverse lazy ranges for H = 16 (every q < 2^60, so values up to 16q fit), in units of q: the
-// range of element j before local stage k of a GS round whose inputs are below 3q.  Both elements of
-// a pair (j, j | 1 << b) share it (ranges depend only on the bits already processed).  The
-// difference leaves below 3q (Shoup); the sum leaves unreduced, below 2r q, except that a pair at
-// r = 12 is first reduced to 6 (2r <= 12 < 16).  Per 16-element round: 8 conditional subtractions
-// in the stages + 12 at the end (back below 3q for the exchange) instead of 32.
-constexpr int gs_red(int r) { return r > 8 ? 6 : r; }
+// Inverse lazy ranges for H = 16 (lz16 contexts: values up to 16q fit, top_bits applies), in
+// units of q: the range of element j before local stage k of a GS round whose inputs are below 3q.
+// Both elements of a pair (j, j | 1 << b) share it (ranges depend only on the bits already
+// processed).  The difference leaves below 3q (Shoup); the sum leaves unreduced, below 2r q, except
+// that a pair at r = 12 is first taken below 2q by top_bits.  Per 16-element round: 6 reductions
+// in the stages + 8 at the end (every element above 3q back below 2q for the exchange) instead of
+// 32 conditional subtractions.
+constexpr int gs_red(int r) { return r > 8 ? 2 : r; }
 constexpr int gs_in(int j, int k) {
   int r = 3;
   for (int b = 0; b < k; ++b) r = ((j >> b) & 1) ? 3 : 2 * gs_red(r);
@@ -334,6 +345,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
     // CT: X-operands below r q (the static range of this stage, fwd_range), reduced by H/2 q
     // only when the stage would outgrow H q; v = w x[jj] in [0, 3q); outputs below (r' + 3) q
     const u64 qh = (u64)(H / 2) * q;
+    const u32 sb = 64 - __builtin_clzll(q);  // bitlength of q (H = 16 top-bits reductions)
     static_for<0, KB>([&](auto sc) {
       constexpr int done = decltype(sc)::value;
       constexpr int b = KB - 1 - done;
@@ -346,7 +358,8 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         if (j & (1 << b)) continue;
         const int jj = j | (1 << b);
         const ulonglong2 w = twiddle(b, j, bitpos, st);
-        u64 u = reduce ? csubk(x[j], qh) : x[j];
+        u64 u = x[j];
+        if constexpr (reduce) u = H == 16 ? top_bits(u, sb, nq) : csubk(u, qh);
         FHE_OPAQUE(u);  // keeps 2u + 3q one v_lshl_add_u64 (not distributed over the select)
         // u + v straight out of the remainder chain; u - v + 3q = (2u + 3q) - (u + v)
         u64 s = shoup_q3_add<GATHER>(x[jj], w.x, w.y, nq, u);
@@ -361,13 +374,15 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       // from below r_out q down to [0, q) (kFinalFwd) or [0, 2q) (kFinalFwd2) by halving steps
       constexpr int rout = fwd_range(RIN, KB, H);
       constexpr int stop = FIN == kFinalFwd ? 1 : 2;
-      // q in [2^60 - 2^56, 2^60) (wave-uniform test; the default moduli are the largest primes
-      // below 2^60): x - (x >> 60) q < 2q for any x < 16 q, one estimate instead of up to three
-      // halving steps (k = x >> 60 <= x / q, and x - k q < x (2^60 - q) / 2^60 + q < 2q)
-      if (rout > 4 && rout <= 16 && (q >> 56) == 15) {
+      // a modulus within 1/16 below 2^s (s = its bitlength: every lz16 modulus; for H = 8, s = 60
+      // is tested): one top-bits estimate instead of up to three halving steps.  Kept a
+      // wave-uniform runtime test even where H = 16 guarantees it: with the branch resolved at
+      // compile time the fused HomMult kernel's allocation spills 31 VGPRs (2 with the branch).
+      const u32 sf = H == 16 ? sb : 60;
+      if (rout > 4 && rout <= 16 && (q >> (sf - 4)) == 15) {
 #pragma unroll
         for (int j = 0; j < E; ++j) {
-          x[j] += (u64)(u32)(x[j] >> 60) * nq;  // x - k q (mod 2^64, exact: the result is >= 0)
+          x[j] = top_bits(x[j], sf, nq);
           if constexpr (FIN == kFinalFwd) x[j] = csubk(x[j], q);
         }
       } else {
@@ -405,8 +420,11 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
   } else if constexpr (H == 16) {
     // GS with lazy sums (gs_in): inputs in [0, 3q); each pair at r q: sum u + v below 2r q,
     // (u - v + r q) w -> [0, 3q); the round ends with every element back in [0, 3q)
-    u64 q6 = 6 * q;
+    const u32 sb = 64 - __builtin_clzll(q);  // bitlength of q (top_bits)
+    u64 q4 = 4 * q, q6 = 6 * q, q8 = 8 * q;
+    asm("" : "+s"(q4));
     asm("" : "+s"(q6));
+    asm("" : "+s"(q8));
     constexpr bool kLast = FIN == kFinalInv || FIN == kFinalInvS30;
     static_for<0, KB>([&](auto bc) {
       constexpr int b = decltype(bc)::value;
@@ -419,10 +437,12 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
           constexpr int r = gs_in(j, b), rr = gs_red(r);
           u64 u = x[j], v = x[jj];
           if constexpr (rr != r) {
-            u = csubk(u, q6);
-            v = csubk(v, q6);
+            u = top_bits(u, sb, nq);
+            v = top_bits(v, sb, nq);
           }
-          const u64 sum = u + v, dif = u - v + (rr == 3 ? q3 : q6);
+          static_assert(rr == 2 || rr == 3 || rr == 4 || rr == 6 || rr == 8, "GS range");
+          const u64 off = rr == 2 ? q2 : rr == 3 ? q3 : rr == 4 ? q4 : rr == 6 ? q6 : q8;
+          const u64 sum = u + v, dif = u - v + off;
           if constexpr (kLast && st == 0) {
             // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
             x[j] = csubk(csubk(shoup_q3<GATHER>(sum, nf0.x, nf0.y, nq), q2), q);
@@ -443,9 +463,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
     } else {
       static_for<0, E>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        constexpr int r = gs_in(j, KB);
-        if constexpr (r > 6) x[j] = csubk(x[j], q6);
-        if constexpr (r > 3) x[j] = csubk(x[j], q3);
+        if constexpr (gs_in(j, KB) > 3) x[j] = top_bits(x[j], sb, nq);
       });
     }
   } else {
@@ -700,7 +718,12 @@ struct Geo {
 // vmcnt retires in issue order, so every twiddle wait also waited for the prefetch, and the
 // prefetch registers pushed the column kernel into spills -- DESIGN.md §8.)
 // FI: the inverse's final stage (kFinalInv, or kFinalInvS30 for split30 outputs).
-template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false, int FI = kFinalInv>
+// R0: the forward's input range (units of q) its lazy schedule starts from.  The row pass that
+// follows must assume the same R0: fwd_range is not monotonic in it (an earlier reduction can leave
+// a smaller bound), so the key-switch / rescale row kernels, which assume 2 (k_modup_col's
+// outputs), get column passes scheduled from 2 as well (col_fwd_pass, k_rescale_col).
+template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false, int FI = kFinalInv,
+          int R0 = 1>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_ntt_col(
     const u64* __restrict__ src, const u64* __restrict__ src2, u64* __restrict__ dst, u32 nlimbs,
     u32 limb0, PolyMap pm, u32 items, const ulonglong2* __restrict__ tw_all,
@@ -737,7 +760,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 
     nf0 = nfold[4 * limb];
     nf1 = nfold[4 * limb + 1];
   }
-  pass_run<G::N1, FWD, FWD ? kNotFinal : FI, kBlockSync, false, H, 1>(
+  pass_run<G::N1, FWD, FWD ? kNotFinal : FI, kBlockSync, false, H, R0>(
       x, GView<G::R2, false, NTS>{dst + pm.dst(p) + loc, sub}, lv, t, tw_all + (u64)limb * N, 1u,
       mods[limb].q, nf0, nf1);
 }
@@ -1443,7 +1466,8 @@ k_rescale_col(const u64* __restrict__ last, u64* __restrict__ dst, u32 nq, u32 i
   const u64 h = ml.q >> 1, mh = mi.q - half[l];
 #pragma unroll
   for (int j = 0; j < kE; ++j) x[j] = csub(reduce_word(csub(x[j] + h, ml.q), mi) + mh, mi.q);
-  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 1>(
+  // scheduled from 2 (inputs are below q): the range k_moddown_row assumes
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2>(
       x, GView<G::R2>{dst + (u64)pl * N + col, sub}, lv, t, tw_all + (u64)l * N, 1u, mi.q,
       {0, 0}, {0, 0});
 }
@@ -1477,7 +1501,8 @@ void col_fwd_pass(const fhe_ctx* c, const u64* src, u64 sp, u64* dst, u64 dp, u3
   using G = Geo<LOGN>;
   const u64 ic = (u64)polys * nlimbs * G::TILES_C;
   const PolyMap pm{1, sp, 0, dp, 0, 0};
-  k_ntt_col<LOGN, true, HD><<<item_grid(ic),
+  // scheduled from 2: the row kernels that follow (k_ks_row_inner, k_moddown_row) assume it
+  k_ntt_col<LOGN, true, HD, false, false, kFinalInv, 2><<<item_grid(ic),
                               G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic,
                                                 c->d_tw_fwd, c->d_nfold, c->d_mods);
 }

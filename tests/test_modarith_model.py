@@ -130,14 +130,46 @@ def test_folded_ct_butterfly(q, H):
         ws = (w << 64) // q
         y = rng.randrange(H * q)
         x = rng.randrange(H * q)
-        u = csub_fast(x, (H // 2) * q) if x + 3 * q > H * q else x
-        assert u == (x - (H // 2) * q if x >= (H // 2) * q and x + 3 * q > H * q else x)
+        if x + 3 * q > H * q:
+            if H == 16:  # lz16: the top-bits estimate (ntt.hip top_bits)
+                u = top_bits(x, q)
+                assert u < 2 * q and (u - x) % q == 0
+            else:
+                u = csub_fast(x, (H // 2) * q)
+                assert u == (x - (H // 2) * q if x >= (H // 2) * q else x)
+        else:
+            u = x
         s = shoup_q3_add(y, w, ws, q, u)
         v = shoup_q3(y, w, ws, q)
         assert s == u + v and s < H * q
         o2 = ((u << 1) + 3 * q - s) & M64
         assert o2 == u - v + 3 * q and o2 < H * q
         assert (s - (x + w * y)) % q == 0 and (o2 - (x - w * y)) % q == 0
+
+
+def top_bits(x, q):
+    """ntt.hip top_bits: x + (x >> s) (-q) mod 2^64, s = bitlength(q)."""
+    s = q.bit_length()
+    return (x + ((x >> s) & M32) * ((-q) & M64)) & M64
+
+
+def _lz16(q):
+    """context.cpp: q < 2^60 within 1/16 below a power of two."""
+    s = q.bit_length()
+    return q < 1 << 60 and q >= (1 << s) - (1 << (s - 4))
+
+
+@pytest.mark.parametrize("bits", [20, 31, 32, 33, 40, 50, 55, 59, 60])
+def test_top_bits_reduction(bits):
+    """For every lz16 modulus and x < 16 q: top_bits(x) < 2q, congruent to x (the forward CT
+    reductions and the final forward reduction of H = 16 kernels)."""
+    rng = random.Random(bits)
+    qs = pyoracle.gen_moduli(10, 2, bits=bits) + [(1 << bits) - (1 << (bits - 4)) + 1]
+    for q in qs:
+        assert _lz16(q)
+        for x in [0, q - 1, q, 2 * q - 1, 8 * q, 16 * q - 1] + [rng.randrange(16 * q) for _ in range(3000)]:
+            r = top_bits(x, q)
+            assert 0 <= r < 2 * q and (r - x) % q == 0, (q, x)
 
 
 def final_top_bits(x, q):
@@ -364,7 +396,7 @@ def test_keyswitch_inner_product_dot(q):
 
 
 def gs_red(r):
-    return 6 if r > 8 else r
+    return 2 if r > 8 else r
 
 
 def gs_in(j, k):
@@ -375,14 +407,14 @@ def gs_in(j, k):
     return r
 
 
-@pytest.mark.parametrize("q", [m for m in _moduli() if m < 1 << 60])
+@pytest.mark.parametrize("q", [m for m in _moduli() if _lz16(m)])
 def test_lazy_gs_round(q):
-    """round_compute's H = 16 inverse (q < 2^60): a 16-element GS round with unreduced sums, the
-    pair reduction at r = 12 and the end-of-round subtractions.  Every value stays below its static
-    range (so below 12q < 2^64), the round leaves [0, 3q), and the outputs are congruent to the
-    exact GS butterflies' (sum, (u - v) w) on the same inputs and twiddles."""
+    """round_compute's H = 16 inverse (lz16 q): a 16-element GS round with unreduced sums, the pair
+    reduction at r = 12 and the end-of-round reductions by top_bits.  Every value stays below its
+    static range (so below 16q <= 2^64), the round leaves [0, 3q), and the outputs are congruent to
+    the exact GS butterflies' (sum, (u - v) w) on the same inputs and twiddles."""
     rng = random.Random(q + 7)
-    q3, q6 = 3 * q, 6 * q
+    q3 = 3 * q
     for trial in range(300):
         # worst-case-heavy inputs below 3q
         x = [rng.choice([0, q3 - 1, rng.randrange(q3)]) for _ in range(16)]
@@ -394,23 +426,21 @@ def test_lazy_gs_round(q):
                     continue
                 jj = j | (1 << b)
                 r = gs_in(j, b)
-                assert gs_in(jj, b) == r
+                assert gs_in(jj, b) == r and r <= 16
                 assert x[j] < r * q and x[jj] < r * q
                 u, v = x[j], x[jj]
                 rr = gs_red(r)
                 if rr != r:
-                    u, v = csub_fast(u, q6), csub_fast(v, q6)
+                    u, v = top_bits(u, q), top_bits(v, q)
                     assert u < rr * q and v < rr * q
                 w = tw[(b, j)]
                 s, d = u + v, u - v + rr * q
-                assert s < 16 * q and 0 < d < 16 * q and s <= M64
+                assert s <= 16 * q and 0 < d < 16 * q and s <= M64
                 x[j], x[jj] = s, shoup_q3(d, w, (w << 64) // q, q)
                 ref[j], ref[jj] = (ref[j] + ref[jj]) % q, (ref[j] - ref[jj]) * w % q
         for j in range(16):
             r = gs_in(j, 4)
             assert x[j] < r * q
-            if r > 6:
-                x[j] = csub_fast(x[j], q6)
             if r > 3:
-                x[j] = csub_fast(x[j], q3)
+                x[j] = top_bits(x[j], q)
             assert x[j] < q3 and x[j] % q == ref[j]

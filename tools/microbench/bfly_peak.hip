@@ -4,11 +4,11 @@
 // Runs the exact butterfly instruction sequences of csrc/ntt.hip round_compute in the row passes
 // (the lazy forms with the mad-chain remainder, shoup_q3<true>; headroom H = 16) on
 // register-resident data at full occupancy, with no memory traffic:
-//   forward  Cooley-Tukey, folded X-operand (shoup_q3_add), the 8q reduction every other stage
-//            (the row passes' schedule), outputs s and (2u + 3q) - s;
+//   forward  Cooley-Tukey, folded X-operand (shoup_q3_add), one top-bits reduction per 4-stage
+//            round (the lz16 row passes' schedule: two per 8-stage pass), outputs s and (2u + 3q) - s;
 //   inverse  Gentleman-Sande with lazy sums (round_compute's H = 16 form, gs_in ranges): sums
-//            unreduced, a pair at 12q reduced to 6q first, (u - v + r q) w by shoup_q3, and the
-//            round's end subtractions back below 3q.
+//            unreduced, a pair at 12q taken below 2q by top_bits first, (u - v + r q) w by
+//            shoup_q3, and the round's end reductions back below 3q.
 // Each thread holds kE = 16 values and runs 4-stage rounds on them exactly as a kernel round does
 // (8 butterflies per stage), with 8 twiddle pairs in registers standing in for the round's
 // gathered twiddles.  The result is the chip's butterflies/s ceiling for that arithmetic, measured
@@ -36,11 +36,16 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // ntt.hip gs_red / gs_in (the static per-element ranges of a lazy GS round)
-constexpr int gs_red(int r) { return r > 8 ? 6 : r; }
+constexpr int gs_red(int r) { return r > 8 ? 2 : r; }
 constexpr int gs_in(int j, int k) {
   int r = 3;
   for (int b = 0; b < k; ++b) r = ((j >> b) & 1) ? 3 : 2 * gs_red(r);
   return r;
+}
+
+// ntt.hip top_bits
+__device__ __forceinline__ u64 top_bits(u64 x, u32 s, u64 nq) {
+  return x + (u64)(u32)(x >> s) * nq;
 }
 
 __device__ __forceinline__ u64 csubk(u64 x, u64 m) {
@@ -61,9 +66,13 @@ __global__ __launch_bounds__(kThreads) void k_bfly_peak(u64* __restrict__ out,
 #pragma unroll
   for (int k = 0; k < 8; ++k) w[k] = tw[(gid + k) & 63];
   const u64 nq = 0 - q;
-  u64 q3 = 3 * q, q6 = 6 * q;
+  u64 q3 = 3 * q, q2 = 2 * q, q4 = 4 * q, q6 = 6 * q, q8 = 8 * q;
   asm("" : "+s"(q3));
+  asm("" : "+s"(q2));
+  asm("" : "+s"(q4));
   asm("" : "+s"(q6));
+  asm("" : "+s"(q8));
+  const u32 sb = 64 - __builtin_clzll(q);
   for (u32 r = 0; r < rounds; ++r) {
     if constexpr (INV) {
       static_for<0, 4>([&](auto bc) {
@@ -76,10 +85,11 @@ __global__ __launch_bounds__(kThreads) void k_bfly_peak(u64* __restrict__ out,
             const ulonglong2 t = w[(j + b) & 7];
             u64 u = x[j], v = x[jj];
             if constexpr (rr != ri) {
-              u = csubk(u, q6);
-              v = csubk(v, q6);
+              u = top_bits(u, sb, nq);
+              v = top_bits(v, sb, nq);
             }
-            const u64 sum = u + v, dif = u - v + (rr == 3 ? q3 : q6);
+            const u64 off = rr == 2 ? q2 : rr == 3 ? q3 : rr == 4 ? q4 : rr == 6 ? q6 : q8;
+            const u64 sum = u + v, dif = u - v + off;
             x[j] = sum;
             x[jj] = fhe::shoup_q3<true>(dif, t.x, t.y, nq);
           }
@@ -87,9 +97,7 @@ __global__ __launch_bounds__(kThreads) void k_bfly_peak(u64* __restrict__ out,
       });
       static_for<0, kE>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        constexpr int ri = gs_in(j, 4);
-        if constexpr (ri > 6) x[j] = csubk(x[j], q6);
-        if constexpr (ri > 3) x[j] = csubk(x[j], q3);
+        if constexpr (gs_in(j, 4) > 3) x[j] = top_bits(x[j], sb, nq);
       });
       continue;
     }
@@ -101,7 +109,8 @@ __global__ __launch_bounds__(kThreads) void k_bfly_peak(u64* __restrict__ out,
         const int jj = j | (1 << b);
         const ulonglong2 t = w[(j + b) & 7];
         if constexpr (!INV) {
-          u64 u = (b & 1) ? csubk(x[j], 8 * q) : x[j];
+          u64 u = x[j];
+          if (b == 1) u = top_bits(u, sb, nq);  // one per round, as in an lz16 row pass
           FHE_OPAQUE(u);
           u64 s = fhe::shoup_q3_add<true>(x[jj], t.x, t.y, nq, u);
           FHE_OPAQUE(s);
