@@ -48,10 +48,23 @@ def _chain(fc, name):
         return [g(63, 1)[0], g(60, 1)[0], g(55, 1)[0], g(62, 1)[0]], [g(61, 1)[0], g(50, 1)[0]]
     if name == "mixed-narrow":  # below 2^60 with and without the top-bits final reduction
         return [g(60, 1)[0], g(50, 1)[0], g(59, 1)[0], g(55, 1)[0]], [g(60, 1, 1)[0], g(45, 1)[0]]
+    if name == "far":  # below 2^60 but not within 1/16 below a power of two: the 8q kernels
+        fr = [0.70, 0.80, 0.90, 0.60, 0.75, 0.85]
+        m = [_prime_below(int(f * (1 << b))) for f, b in zip(fr, [59, 56, 50, 58, 57, 52])]
+        return m[:L], m[L:]
     raise ValueError(name)
 
 
-CHAINS = ["b50", "b55", "b60", "b61", "b62", "b63", "mixed-wide", "mixed-narrow"]
+def _prime_below(bound):
+    """Largest prime q < bound with q = 1 mod 2N (N = 2^LOG_N)."""
+    step = 2 << LOG_N
+    q = (bound - 1) // step * step + 1
+    while not pyoracle.is_prime(q):
+        q -= step
+    return q
+
+
+CHAINS = ["b50", "b55", "b60", "b61", "b62", "b63", "mixed-wide", "mixed-narrow", "far"]
 _CTX = {}
 
 
@@ -68,7 +81,7 @@ def test_chain_ntt_and_hommult(fc, name):
     qs = ctx.moduli
     top = max(ctx.all_moduli).bit_length()
     assert top == {"b50": 50, "b55": 55, "b60": 60, "b61": 61, "b62": 62, "b63": 63,
-                   "mixed-wide": 63, "mixed-narrow": 60}[name]
+                   "mixed-wide": 63, "mixed-narrow": 60, "far": 59}[name]
     x = rand(qs, LOG_N, (3,), seed=1)
     t = fc.to_device(x)
     ctx.ntt_(t)
@@ -116,7 +129,7 @@ def test_chain_vec_baseconv_keyswitch(fc, name):
         assert (h0[i] == r0).all() and (h1[i] == r1).all(), i
 
 
-@pytest.mark.parametrize("name", ["b55", "b62", "b63", "mixed-wide"])
+@pytest.mark.parametrize("name", ["b55", "b62", "b63", "mixed-wide", "far"])
 def test_chain_rescale_and_keys(fc, name):
     ctx = ctx_for(fc, name)
     qs, ps = ctx.moduli, ctx.special
