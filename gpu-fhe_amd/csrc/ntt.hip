@@ -444,9 +444,10 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
           const u64 off = rr == 2 ? q2 : rr == 3 ? q3 : rr == 4 ? q4 : rr == 6 ? q6 : q8;
           const u64 sum = u + v, dif = u - v + off;
           if constexpr (kLast && st == 0) {
-            // last stage of the whole inverse: fold N^-1 (both outputs) and reduce to [0, q)
-            x[j] = csubk(csubk(shoup_q3<GATHER>(sum, nf0.x, nf0.y, nq), q2), q);
-            x[jj] = csubk(csubk(shoup_q3<GATHER>(dif, nf1.x, nf1.y, nq), q2), q);
+            // last stage of the whole inverse: fold N^-1 (both outputs) by the exact-quotient
+            // product ([0, 2q)) and reduce to [0, q)
+            x[j] = csubk(shoup_fast(sum, nf0.x, nf0.y, nq), q);
+            x[jj] = csubk(shoup_fast(dif, nf1.x, nf1.y, nq), q);
           } else {
             const ulonglong2 w = twiddle(b, j, bitpos, st);
             x[j] = sum;
