@@ -326,13 +326,17 @@ def run_vec(args, world, rank):
     gen.manual_seed(5 + rank)
     mods = ctx.moduli[shard.lo:shard.hi]
     polys = 2 * args.batch
-    a = uniform_limbs(gen, mods, (polys,), n)
-    b = uniform_limbs(gen, mods, (polys,), n)
-    out = torch.empty_like(a)
+    # one (a, b, out) set per operator, 384 MiB each at the default shape: an operator's inputs
+    # were last touched two operators (768 MiB) earlier, so they stream from HBM rather than from
+    # the 256 MB Infinity Cache
+    sets = []
+    for _ in range(3):
+        a = uniform_limbs(gen, mods, (polys,), n)
+        sets.append((a, uniform_limbs(gen, mods, (polys,), n), torch.empty_like(a)))
     lib = load()
 
     def step():
-        for fn in (lib.fhe_vec_add, lib.fhe_vec_sub, lib.fhe_vec_mul):
+        for fn, (a, b, out) in zip((lib.fhe_vec_add, lib.fhe_vec_sub, lib.fhe_vec_mul), sets):
             check(fn(ctx.handle, out.data_ptr(), a.data_ptr(), b.data_ptr(), polys, shard.lo,
                      shard.nlimbs, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
                   "fhe_vec")
