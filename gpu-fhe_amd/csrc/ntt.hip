@@ -1450,16 +1450,23 @@ k_rescale_col(const u64* __restrict__ last, u64* __restrict__ dst, u32 nq, u32 i
   const LViewC<G::SUBS_C> lv{lds + sub};
   const u32 it = blockIdx.x;
   if (it >= items) return;
-  u32 tile, pl;  // XCD-grouped placement as in k_ntt_col
-  if ((items / G::TILES_C) % 8 == 0) {
+  // placement: with 8 | polys, XCD x takes the polys p = x mod 8 and runs the nq limbs of one
+  // (p, tile) back to back, so last's column tile comes from HBM once and from the XCD's L2 for
+  // the other limbs; otherwise limbs fastest over all XCDs
+  const u32 polys = items / (nq * G::TILES_C);
+  u32 tile, l, p;
+  if (polys % 8 == 0) {
     const u32 k = it / 8;
-    tile = k % G::TILES_C;
-    pl = (k / G::TILES_C) * 8 + it % 8;
+    l = k % nq;
+    tile = (k / nq) % G::TILES_C;
+    p = (k / (nq * G::TILES_C)) * 8 + it % 8;
   } else {
-    tile = it % G::TILES_C;
-    pl = it / G::TILES_C;
+    l = it % nq;
+    tile = (it / nq) % G::TILES_C;
+    p = it / (nq * G::TILES_C);
   }
-  const u32 l = __builtin_amdgcn_readfirstlane(pl % nq), p = pl / nq;
+  l = __builtin_amdgcn_readfirstlane(l);
+  const u32 pl = p * nq + l;
   const u64 col = (u64)tile * G::SUBS_C;
   u64 x[kE];
   pass_load<G::N1, true>(GView<G::R2>{const_cast<u64*>(last) + (u64)p * N + col, sub}, t, x);
