@@ -21,8 +21,10 @@ __device__ __forceinline__ u64 op_canon(int op, u64 a, u64 b, const ModParams& m
 }
 
 // One poly-limb row per blockIdx.y (its ModParams uniform, no per-element limb division), kU
-// 16-byte pairs per lane per operand issued back to back.  Rows beyond the grid's y extent loop.
-constexpr int kU = 4;
+// 16-byte pairs per lane per operand.  Rows beyond the grid's y extent loop.  kU = 1 measured best
+// (bench --workload vec, same-box: 1 / 2 / 4 / 8 -> 2.32 / 2.28 / 2.17 / 2.00 e11 coeff-op/s):
+// more, shorter workgroups keep more loads in flight than more loads per lane.
+constexpr int kU = 1;
 template <int OP>
 __global__ __launch_bounds__(kThreads) void k_vec_ctx(u64* __restrict__ out,
                                                       const u64* __restrict__ a,
