@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch", "mulrelin", "ntt-batch",
-                                           "vec"],
+                                           "vec", "rotate"],
                     default="hommult")
     ap.add_argument("--batch", type=int, default=None,
                     help="ciphertexts per GPU per step (default 64 for hommult -- the throughput "
@@ -588,6 +588,45 @@ def run_mulrelin(args, world, rank):
     return out_line, None
 
 
+def run_rotate(args, world, rank):
+    """Hoisted rotations (fhe_rotate_hoisted, a widening beyond SURVEY §8f row 1): R Galois
+    elements of the same ciphertexts sharing one ModUp, at the key-switch configuration
+    (N = 2^16, L = 16, K = 4, dnum = 4), batch B per call.  `value` counts rotations (B R per
+    step); the same R rotations through R fhe_rotate calls are timed beside it."""
+    L, K, dnum, R = 16, 4, 4, 8
+    n = 1 << args.log_n
+    ctx = fc.Context(args.log_n, L=L, K=K, dnum=dnum)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(13 + rank)
+    B = args.batch
+    ct = uniform_limbs(gen, ctx.moduli, (B, 2), n)
+    keys = [(uniform_limbs(gen, ctx.all_moduli, (dnum,), n),
+             uniform_limbs(gen, ctx.all_moduli, (dnum,), n)) for _ in range(R)]
+    elts = [ctx.galois_elt(r) for r in range(1, R + 1)]
+    lib = load()
+    ws = ctx.workspace(max(lib.fhe_rotate_hoisted_workspace(ctx.handle, B),
+                           lib.fhe_rotate_workspace(ctx.handle, B)))
+    out = torch.empty(R, B, 2, L, n, dtype=torch.int64, device="cuda")
+    hoisted = lambda: ctx.rotate_hoisted(ct, elts, keys, workspace=ws, out=out)  # noqa: E731
+
+    def plain():
+        for r in range(R):
+            ctx.rotate(ct, elts[r], keys[r][0], keys[r][1], workspace=ws)
+
+    dt, kavg = timed(hoisted, args, world, 64)
+    dt_plain, _ = timed(plain, args, world, 1)
+    per_s = B * R * args.steps * world / dt
+    return {"metric": "hoisted rotations/sec at N=2^16, L=16, K=4, dnum=4 (8 Galois elements per ModUp)",
+            "value": round(per_s, 2), "unit": "rotations/s",
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "config": {"workload": "hoisted rotations (fhe_rotate_hoisted)", "log_n": args.log_n,
+                       "L": L, "K": K, "dnum": dnum, "rotations_per_modup": R, "batch": B,
+                       "parallelism": f"replicas x{world}"},
+            "unhoisted_rotations_per_sec": round(B * R * args.steps * world / dt_plain, 2),
+            "hoisting_speedup": round(dt_plain / dt, 3),
+            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()}}, None
+
+
 def main():
     # stdout carries exactly one JSON line: anything else the libraries print there (RCCL prints
     # its version banner to stdout when a communicator comes up) is sent to stderr
@@ -599,7 +638,7 @@ def main():
         args.batch = 64 if args.workload == "hommult" else 16
     world, rank = dist_setup(args)
     run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch, "vec": run_vec,
-           "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch}[args.workload]
+           "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch, "rotate": run_rotate}[args.workload]
     out, cpu = run(args, world, rank)
     if rank == 0:
         line = {"metric": out.pop("metric"), "value": out.pop("value"), "unit": out.pop("unit"),

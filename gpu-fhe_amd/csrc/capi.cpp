@@ -311,6 +311,29 @@ int fhe_rotate(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t gal
   return launch_rotate(c, out, in, galois_elt, rot_b, rot_a, batch, ws, hs(s));
 }
 
+size_t fhe_rotate_hoisted_workspace(const fhe_ctx* c, uint32_t batch) {
+  return c ? rotate_hoisted_workspace_bytes(c, batch) : 0;
+}
+
+int fhe_rotate_hoisted(const fhe_ctx* c, uint64_t* out, const uint64_t* in,
+                       const uint32_t* galois_elts, const uint64_t* const* rot_b,
+                       const uint64_t* const* rot_a, uint32_t count, uint32_t batch, void* ws,
+                       fhe_stream_t s) {
+  int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_rotate_hoisted");
+  if (rc) return rc;
+  if (count && (!galois_elts || !rot_b || !rot_a)) {
+    set_error("fhe_rotate_hoisted: null Galois element or key array");
+    return kInvalid;
+  }
+  const uint64_t span = (uint64_t)count * batch * 2 * c->L * c->n;
+  if (span && in < out + span && out < in + (uint64_t)batch * 2 * c->L * c->n) {
+    set_error("fhe_rotate_hoisted: out must not overlap in");
+    return kInvalid;
+  }
+  if ((rc = ensure_ws(c, rotate_hoisted_workspace_bytes(c, batch), &ws, hs(s)))) return rc;
+  return launch_rotate_hoisted(c, out, in, galois_elts, rot_b, rot_a, count, batch, ws, hs(s));
+}
+
 size_t fhe_mul_relin_workspace(const fhe_ctx* c, uint32_t batch) {
   return c ? mul_relin_workspace_bytes(c, batch) : 0;
 }

@@ -240,4 +240,68 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
                                 &ep);
 }
 
+size_t rotate_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch) {
+  // c1 (NTT form) and its coefficient form, sigma(c0) [batch][L][N], then the key-switch workspace
+  // (its ext region holds the NTT-form digits across the rotations)
+  // (+ [2 batch][K][N] for the fused ModDown's INTT output)
+  return (3 * (size_t)c->L + 2 * (size_t)c->K) * batch * c->n * sizeof(u64) +
+         keyswitch_workspace_bytes(c, c->L, batch);
+}
+
+// Hoisted rotations (Halevi-Shoup): the ModUp of c1 -- INTT, base conversion, NTT of every digit,
+// the bulk of a key-switch -- runs once, and each rotation reads the NTT-form digits through its
+// automorphism inside the inner product (sigma commutes with the digit decomposition up to the
+// conversion's multiples of the digit modulus, which the key-switch tolerates either way).  Per
+// rotation: sigma(c0), the gathered inner product, ModDown with sigma(c0) added in its finish.
+// Restated by oracle/pyoracle.py rotate_hoisted; decrypts to sigma_k(m) like fhe_rotate, but is
+// not bit-identical to it (ModUp of sigma(c1) vs sigma of ModUp(c1)).
+int launch_rotate_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* galois,
+                          const u64* const* rot_b, const u64* const* rot_a, u32 count, u32 batch,
+                          void* ws, hipStream_t s) {
+  if (c->K == 0) {
+    set_error("rotate_hoisted: context has no special primes (K = 0)");
+    return kInvalid;
+  }
+  const u32 two_n = 2u << c->log_n;
+  for (u32 r = 0; r < count; ++r)
+    if ((galois[r] & 1) == 0 || galois[r] >= two_n) {
+      set_error("rotate_hoisted: every Galois element must be odd and below 2N");
+      return kInvalid;
+    }
+  if (batch == 0 || count == 0) return kOk;
+  const u32 L = c->L;
+  const u64 n = c->n, ln = (u64)L * n;
+  u64* c1 = static_cast<u64*>(ws);  // [batch][L][N] NTT form
+  u64* c_all = c1 + batch * ln;     // [batch][L][N] coefficient form
+  u64* sc0 = c_all + batch * ln;    // [batch][L][N]
+  u64* ydn = sc0 + batch * ln;      // [2 batch][K][N]
+  u64* kws = ydn + 2 * batch * (u64)c->K * n;
+  FHE_HIP_CHECK(hipMemcpy2DAsync(c1, ln * sizeof(u64), in + ln, 2 * ln * sizeof(u64),
+                                 ln * sizeof(u64), batch, hipMemcpyDeviceToDevice, s));
+  int rc;
+  if ((rc = launch_ntt_strided(c, false, c1, ln, c_all, ln, batch, 0, L, s))) return rc;
+  const CAll call = CAll::contiguous(c_all, L, n);
+  KsHoist up;
+  up.modup_only = true;
+  if ((rc = launch_keyswitch_shard(c, nullptr, nullptr, call, c1, nullptr, nullptr, 0, L, batch,
+                                   kws, s, nullptr, &up)))
+    return rc;
+  for (u32 r = 0; r < count; ++r) {
+    u64* o = out + (u64)r * batch * 2 * ln;
+    if ((rc = launch_automorphism(c, sc0, ln, in, 2 * ln, batch, 0, L, galois[r], true, s)))
+      return rc;
+    KsHoist h;
+    h.galois = galois[r];
+    h.ydn = ydn;
+    KsEpilogue ep;
+    ep.out_bs = 2 * ln;
+    ep.add0 = sc0;
+    ep.add_bs = ln;
+    if ((rc = launch_keyswitch_shard(c, o, o + ln, call, c1, rot_b[r], rot_a[r], 0, L, batch, kws,
+                                     s, &ep, &h)))
+      return rc;
+  }
+  return kOk;
+}
+
 }  // namespace fhe

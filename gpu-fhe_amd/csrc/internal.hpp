@@ -137,6 +137,14 @@ struct KsEpilogue {
   const u64* add1 = nullptr;
   u64 add_bs = 0;
 };
+// Hoisted rotations (galois.hip launch_rotate_hoisted): modup_only runs ModUp alone and leaves the
+// NTT-form digits in the workspace's ext region; otherwise the key-switch skips ModUp and reads
+// those digits (and d2_own) through sigma_galois inside the inner product (unfused kernels).
+struct KsHoist {
+  bool modup_only = false;
+  u32 galois = 0;
+  u64* ydn = nullptr;  // [2 batch][K][N] scratch for the fused ModDown (the ext region is taken)
+};
 struct ModDownRowArgs {
   const u64* conv;
   u64* ks0;
@@ -212,7 +220,7 @@ inline bool ks_split30(const fhe_ctx* c) { return !c->lz16; }
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
                            u32 nlimbs, u32 batch, void* ws, hipStream_t s,
-                           const KsEpilogue* ep = nullptr);
+                           const KsEpilogue* ep = nullptr, const KsHoist* hoist = nullptr);
 size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch);
 // Fast basis extension between contiguous ctx limb ranges: in [S][N] over limbs [s0, s0+S),
 // out [T][N] over limbs [t0, t0+T) (ranges disjoint).
@@ -232,6 +240,12 @@ size_t rescale_workspace_bytes(const fhe_ctx* c, u32 polys, u32 nl);
 int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, const u64* rot_b,
                   const u64* rot_a, u32 batch, void* ws, hipStream_t s);
 size_t rotate_workspace_bytes(const fhe_ctx* c, u32 batch);
+// `count` rotations of the same ciphertexts sharing one ModUp: out [count][batch][2][L][N],
+// galois[r] with its key rot_b[r] / rot_a[r] (host arrays of device pointers)
+int launch_rotate_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* galois,
+                          const u64* const* rot_b, const u64* const* rot_a, u32 count, u32 batch,
+                          void* ws, hipStream_t s);
+size_t rotate_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch);
 
 // ---- launchers (pipeline.hip): SURVEY.md §8(f) row 4 -----------------------------------
 int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, const u64* evk_b,

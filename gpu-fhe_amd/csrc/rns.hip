@@ -132,11 +132,21 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc, u6
                                                        const u64* __restrict__ evk_a, u32 rows,
                                                        u32 nq, RowMap map, u32 alpha, u32 L,
                                                        u32 batch, u32 log_n,
-                                                       const ModParams* __restrict__ mods) {
+                                                       const ModParams* __restrict__ mods,
+                                                       u32 gal) {
   const u32 r = blockIdx.y;
   const u64 n = 1ull << log_n, rn = (u64)rows * n;
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   const u64 e = (u64)r * n + i;
+  // hoisted rotation (gal != 0): the digits and d2_own are read through sigma_gal's NTT-domain
+  // gather (slot i <- slot brv(((2 brv(i) + 1) gal mod 2N - 1) / 2), galois.hip), the key at i
+  u64 si = i;
+  if (gal) {
+    const u32 sh = 32 - log_n;
+    const u32 g = ((2 * (__builtin_bitreverse32((u32)i) >> sh) + 1) * gal) & ((2u << log_n) - 1);
+    si = __builtin_bitreverse32((g - 1) >> 1) >> sh;
+  }
+  const u64 es = (u64)r * n + si;
   const u32 limb = map.limb(r);
   const ModParams m = mods[limb];
   const u32 own = limb < L ? limb / alpha : 0xffffffffu;
@@ -151,8 +161,8 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc, u6
       u64 s0 = 0, s1 = 0;
 #pragma unroll
       for (int j = 0; j < DNUM; ++j) {
-        const u64 x = (u32)j == own ? d2_own[((u64)b * nq + r) * n + i]
-                                    : ext[((u64)j * batch + b) * rn + e];
+        const u64 x = (u32)j == own ? d2_own[((u64)b * nq + r) * n + si]
+                                    : ext[((u64)j * batch + b) * rn + es];
         const u128 p0 = (u128)x * kb[j], p1 = (u128)x * ka[j];
         s0 = csub(s0 + reduce128_wide((u64)p0, (u64)(p0 >> 64), m), m.q);
         s1 = csub(s1 + reduce128_wide((u64)p1, (u64)(p1 >> 64), m), m.q);
@@ -166,8 +176,8 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc, u6
     u128 s0 = 0, s1 = 0;
 #pragma unroll
     for (int j = 0; j < DNUM; ++j) {
-      const u64 x = (u32)j == own ? d2_own[((u64)b * nq + r) * n + i]
-                                  : ext[((u64)j * batch + b) * rn + e];
+      const u64 x = (u32)j == own ? d2_own[((u64)b * nq + r) * n + si]
+                                  : ext[((u64)j * batch + b) * rn + es];
       s0 += (u128)x * kb[j];
       s1 += (u128)x * ka[j];
     }
@@ -369,7 +379,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const u64* c_al
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
                            u32 nlimbs, u32 batch, void* ws, hipStream_t s,
-                           const KsEpilogue* epi) {
+                           const KsEpilogue* epi, const KsHoist* hoist) {
   if (c->K == 0) {
     set_error("keyswitch: context has no special primes (K = 0)");
     return kInvalid;
@@ -394,7 +404,11 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   // (no NTT-form ext in HBM, no separate inner-product pass); otherwise full NTTs + k_ks_inner.
   // Wide contexts (a modulus >= 2^61) take the unfused kernels: the fused ones rely on lazy
   // ranges and 128-bit sums that need q < 2^61.
-  const bool fused = c->dnum <= 4 && !c->wide;
+  // Hoisted rotations (KsHoist) take the unfused kernels: the digits must exist in NTT form in
+  // HBM so that each rotation's inner product can gather them through its automorphism.
+  const bool fusable = c->dnum <= 4 && !c->wide;
+  const bool fused = !hoist && fusable;
+  const u32 gal = hoist ? hoist->galois : 0;
   // Fused ModUp (with the fused row kernel, digits of <= 4 limbs): the base conversion runs
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
   // digit's source rows; the extended rows are never written in coefficient form.
@@ -403,6 +417,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     set_error("keyswitch: a prepared (pre-scaled) input needs the fused ModUp (ks_prepared)");
     return kInvalid;
   }
+  if (!hoist || hoist->modup_only) {  // ModUp (a hoisted rotation's inner step skips it)
   u64* yws = conv + 2 * B * (u64)nlimbs * n;  // [B][alpha][N]
   auto ntt_fwd = [&](u64* p, u32 l0, u32 nl) {
     return fused ? launch_ntt_col_fwd(c, p, rn, p, rn, batch, l0, nl, s)
@@ -452,6 +467,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     if ((rc = ntt_fwd(e + (u64)nlimbs * n, L, K))) return rc;
   }
   prof_mark(s, "ks_modup");
+  if (hoist) return kOk;  // modup_only: the NTT-form digits stay in the workspace's ext region
+  }
   if (fused) {
     const KsRowArgs ka{acc, acc_ws, ext, B * rn, d2_own, evk_b, evk_a, rows, nlimbs, limb0, L,
                        alpha, L, batch};
@@ -462,7 +479,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
 #define X(k)                                                                                     \
   case k:                                                                                        \
     k_ks_inner<k><<<gi, kThreads, 0, s>>>(acc, acc_ws, ext, d2_own, evk_b, evk_a, rows, nlimbs, \
-                                          map, alpha, L, batch, c->log_n, c->d_mods);           \
+                                          map, alpha, L, batch, c->log_n, c->d_mods, gal);      \
     break;
     X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #undef X
@@ -471,7 +488,9 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   prof_mark(s, "ks_inner");
   // ModDown: INTT the P rows of both accumulators, convert P -> own Q-limbs, NTT, finish
   u64* accp = acc + (u64)nlimbs * n;
-  const bool fused_down = fused && K <= 4 && (u64)c->dnum * rows >= 2 * (u64)K;
+  // (a hoisted rotation's inner step too, with its own scratch for the INTT output)
+  const bool fused_down = K <= 4 && ((fused && (u64)c->dnum * rows >= 2 * (u64)K) ||
+                                     (hoist && hoist->ydn && fusable));
   // Fused ModDown (fused path, K <= 4): the P -> Q conversion runs inside the column-forward
   // pass of the conversion NTT (k_modup_col, as ModUp), on the P rows the INTT has already scaled
   // into the ext region (free once the inner product has run): conv is never written in
@@ -479,7 +498,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   if (fused_down) {
     // the INTT writes y = [x_k (P^_k)^-1]_{p_k} straight into [2 batch][K][N] (its last stage
     // folds N^-1 (P^_k)^-1, c->d_nfold_down): no separate scaling pass
-    u64* ydn = ext;
+    u64* ydn = hoist ? hoist->ydn : ext;
     if ((rc = launch_ntt_strided(c, false, accp, rn, ydn, (u64)K * n, 2 * batch, L, K, s,
                                  c->d_nfold_down, ks_split30(c))))
       return rc;

@@ -334,6 +334,38 @@ class Context:
                                  _ptr(rot_a), batch, _ptr(ws), _stream(ct)), "fhe_rotate")
         return out
 
+    def rotate_hoisted(self, ct, galois_elts, rot_keys, workspace=None, out=None):
+        """Several rotations of the same ct [..., 2, L, N] (NTT form) sharing one ModUp
+        (fhe_rotate_hoisted): galois_elts[r] with rot_keys[r] = (rot_b, rot_a), each
+        [dnum, L + K, N].  Returns [count, ..., 2, L, N]; output r decrypts to sigma_r(m)."""
+        _check_tensor(ct, "ct", (2, self.L, self.n))
+        elts = [int(g) for g in galois_elts]
+        if len(rot_keys) != len(elts):
+            raise ValueError("rotate_hoisted: one key per Galois element")
+        for kb, ka in rot_keys:
+            if tuple(kb.shape) != (self.dnum, self.L + self.K, self.n) or ka.shape != kb.shape:
+                raise ValueError("rotate_hoisted: keys must be [dnum, L + K, N]")
+            if kb.device != ct.device or ka.device != ct.device or not (
+                    kb.is_contiguous() and ka.is_contiguous()):
+                raise ValueError("rotate_hoisted: keys must be contiguous on the ct's device")
+        batch = ct.numel() // (2 * self.L * self.n)
+        count = len(elts)
+        if out is None:
+            out = _empty(count, *ct.shape, dtype=ct.dtype, device=ct.device)
+        elif tuple(out.shape) != (count, *ct.shape) or not out.is_contiguous():
+            raise ValueError("rotate_hoisted: out must be a contiguous [count, ..., 2, L, N] tensor")
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_rotate_hoisted_workspace(self._ptr, batch))
+        g_arr = (ctypes.c_uint32 * max(count, 1))(*elts)
+        b_arr = (ctypes.c_void_p * max(count, 1))(*[kb.data_ptr() for kb, _ in rot_keys])
+        a_arr = (ctypes.c_void_p * max(count, 1))(*[ka.data_ptr() for _, ka in rot_keys])
+        with torch.cuda.device(self.device):
+            check(lib.fhe_rotate_hoisted(self._ptr, _ptr(out), _ptr(ct), g_arr, b_arr, a_arr,
+                                         count, batch, _ptr(ws), _stream(ct)),
+                  "fhe_rotate_hoisted")
+        return out
+
     # ---- SURVEY.md §8(f) row 3: sampling, keys, encryption --------------------------------
     # seed=None draws a fresh 64-bit nonce from the OS CSPRNG.  An explicit seed is for
     # reproducible tests: never reuse one per secret key (fhecore.h SECURITY note).

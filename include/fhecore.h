@@ -201,6 +201,20 @@ int fhe_rotate(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t g
                const uint64_t* rot_b, const uint64_t* rot_a, uint32_t batch, void* workspace,
                fhe_stream_t stream);
 
+/* fhe_rotate_hoisted: `count` rotations of the same ciphertexts sharing one ModUp (hoisting:
+ * the INTT, base conversion and NTT of c1's digits run once; each rotation reads them through
+ * its automorphism inside the inner product).  in [batch][2][L][N] NTT form over Q; out
+ * [count][batch][2][L][N] (must not overlap in); galois_elts[r] with its key rot_b[r], rot_a[r]
+ * ([dnum][L + K][N] device pointers in host arrays, as for fhe_rotate).  Each output decrypts to
+ * sigma_k(m) like fhe_rotate's, but is not bit-identical to it (ModUp of sigma(c1) differs from
+ * sigma of ModUp(c1) by multiples of the digit moduli); restated by oracle/pyoracle.py
+ * rotate_hoisted. */
+size_t fhe_rotate_hoisted_workspace(const fhe_ctx* ctx, uint32_t batch);
+int fhe_rotate_hoisted(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in,
+                       const uint32_t* galois_elts, const uint64_t* const* rot_b,
+                       const uint64_t* const* rot_a, uint32_t count, uint32_t batch,
+                       void* workspace, fhe_stream_t stream);
+
 /* ---- wire format (not in the reference) ------------------------------
  * A self-describing little-endian blob for any [polys][nlimbs][N] residue tensor over context
  * limbs [limb0, limb0 + nlimbs) -- ciphertexts, keys, plaintexts: "FHEC", version 1, flags (bit 0

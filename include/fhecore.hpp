@@ -353,6 +353,36 @@ class Evaluator {
           "fhe_rotate");
     return out;
   }
+  // Several rotations of one ciphertext sharing a single ModUp (fhe_rotate_hoisted); output r
+  // decrypts to sigma_{galois_elts[r]}(m).
+  std::vector<Ciphertext> rotate_hoisted(const Ciphertext& ct, const std::vector<uint32_t>& galois_elts,
+                                         const std::vector<const SwitchKey*>& keys) const {
+    if (ct.components != 2 || !ct.ntt_form || ct.limbs != ctx_.L())
+      throw Error(FHE_EINVAL, "rotate_hoisted: need a 2-component NTT-form ciphertext over L limbs");
+    if (keys.size() != galois_elts.size())
+      throw Error(FHE_EINVAL, "rotate_hoisted: one key per Galois element");
+    const size_t words = (size_t)2 * ct.limbs * ctx_.n(), count = galois_elts.size();
+    DeviceBuffer all(words * (count ? count : 1));
+    std::vector<const uint64_t*> kb(count), ka(count);
+    for (size_t r = 0; r < count; ++r) {
+      kb[r] = keys[r]->b();
+      ka[r] = keys[r]->a();
+    }
+    const size_t need = fhe_rotate_hoisted_workspace(ctx_.get(), 1);
+    if (ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
+    check(fhe_rotate_hoisted(ctx_.get(), all.data(), ct.data(), galois_elts.data(), kb.data(),
+                             ka.data(), (uint32_t)count, 1, ws_.data(), s_),
+          "fhe_rotate_hoisted");
+    std::vector<Ciphertext> out;
+    for (size_t r = 0; r < count; ++r) {
+      out.emplace_back(ctx_, 2, ct.limbs, true);
+      if (hipMemcpyAsync(out.back().data(), all.data() + r * words, words * 8,
+                         hipMemcpyDeviceToDevice, s_) != hipSuccess)
+        throw Error(FHE_EDEVICE, "rotate_hoisted: copy");
+    }
+    if (hipStreamSynchronize(s_) != hipSuccess) throw Error(FHE_EDEVICE, "rotate_hoisted: sync");
+    return out;
+  }
 
  private:
   static void same(const Ciphertext& a, const Ciphertext& b, const char* who) {

@@ -580,6 +580,37 @@ def rotate(ct_ntt, k: int, rot_b, rot_a, qs, ps, dnum, log_n: int):
     return np.stack([(c0 + ks0) % col, ks1 % col])
 
 
+def rotate_hoisted(ct_ntt, ks, keys, qs, ps, dnum, log_n: int):
+    """Hoisted rotations (Halevi-Shoup), restated for gpu-fhe_amd/csrc/galois.hip
+    launch_rotate_hoisted: ModUp(c1) once -- INTT, digit base conversion, NTT of every extended
+    digit -- then per Galois element k with key (rot_b, rot_a): the digits gathered through
+    sigma_k in the NTT domain, the inner product with the key, ModDown, plus sigma_k(c0).
+    Not bit-identical to rotate() (ModUp(sigma c1) differs from sigma ModUp(c1) by multiples of
+    the digit moduli), but decrypts to sigma_k(m) the same way.  Returns [len(ks), 2, L, N]."""
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    allm = qs + ps
+    c1 = np.asarray(ct_ntt[1]).astype(object)
+    ext = [rns_ntt_fwd(e, allm) for e in modup(rns_ntt_inv(c1, qs), qs, ps, dnum)]
+    # the digit's own rows are c1 itself (NTT(INTT(c1)) = c1)
+    for (lo, hi), e in zip(digit_ranges(len(qs), dnum), ext):
+        e[lo:hi] = c1[lo:hi]
+    mods = _mods_col(allm)
+    col = _mods_col(qs)
+    out = []
+    for k, (rot_b, rot_a) in zip(ks, keys):
+        idx = automorphism_ntt_index(k, log_n)
+        acc0 = np.zeros((len(allm), c1.shape[-1]), dtype=object)
+        acc1 = np.zeros_like(acc0)
+        for j, e in enumerate(ext):
+            g = e[..., idx]
+            acc0 = (acc0 + g * np.asarray(rot_b[j]).astype(object)) % mods
+            acc1 = (acc1 + g * np.asarray(rot_a[j]).astype(object)) % mods
+        c0 = automorphism_ntt(ct_ntt[0], k, log_n)
+        out.append(np.stack([(c0 + moddown_ntt(acc0, qs, ps)) % col, moddown_ntt(acc1, qs, ps)]))
+    return np.stack(out)
+
+
 def rescale_coeff(x, moduli):
     """Divide-and-round by the last modulus: x (l, N) coefficient form over q_0..q_{l-1} ->
     (l - 1, N) with out_i = floor((X + q_last // 2) / q_last) mod q_i, X the CRT value in

@@ -141,6 +141,22 @@ int main() {
           return 1;
         }
       }
+      // hoisted: the same rotation and the conjugation from one ModUp
+      const uint32_t kconj = 2 * (uint32_t)kn - 1;
+      const fhe::SwitchKey ck = kg.rotation_key(kconj, 47);
+      const std::vector<fhe::Ciphertext> hs = kev.rotate_hoisted(ct, {k, kconj}, {&rk, &ck});
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t g = h ? kconj : k;
+        const std::vector<int64_t> rh = decrypt_limb0(hs[h]);
+        for (u64 i = 0; i < kn; ++i) {
+          const u64 t = i * g % (2 * kn);
+          const int64_t want = t < kn ? m[i] : -m[i];
+          if (std::llabs(rh[t % kn] - want) > 1000) {
+            std::printf("FAIL hoisted rotation %d coeff %llu\n", h, (unsigned long long)i);
+            return 1;
+          }
+        }
+      }
       const fhe::SwitchKey rl = kg.relin_key(46);
       const fhe::Ciphertext sq = kev.mul_relin(ct, ct, rl, false);
       if (sq.limbs != 3) {

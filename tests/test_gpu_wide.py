@@ -188,3 +188,21 @@ def test_reference_shim_ntt_wide_mod(fc, bits):
     assert (arithmetic.iNTT(y, MOD=q) == x).all()
     naive = pyoracle.ntt_naive([int(v) for v in x], q)
     assert [int(v) for v in y] == list(naive)
+
+
+@pytest.mark.parametrize("name", CHAINS)
+def test_chain_rotate_hoisted(fc, name):
+    """Hoisted rotations on every width class: the wide contexts take the exact unfused kernels
+    end to end, the others the gathered inner product with the fused ModDown."""
+    ctx = ctx_for(fc, name)
+    qs, allm = ctx.moduli, ctx.all_moduli
+    ct = rand(qs, LOG_N, (2, 2), seed=11)
+    ct[0, 0, :, :16] = np.array(qs, dtype=np.uint64)[:, None] - 1
+    keys = [(rand(allm, LOG_N, (DNUM,), seed=12 + 2 * r), rand(allm, LOG_N, (DNUM,), seed=13 + 2 * r))
+            for r in range(2)]
+    ks = [ctx.galois_elt(1), (2 << LOG_N) - 1]
+    got = fc.to_host(ctx.rotate_hoisted(fc.to_device(ct), ks,
+                                        [(fc.to_device(b), fc.to_device(a)) for b, a in keys]))
+    for i in range(2):
+        want = pyoracle.rotate_hoisted(ct[i], ks, keys, qs, ctx.special, DNUM, LOG_N)
+        assert (got[:, i].astype(object) == want).all(), i

@@ -231,6 +231,39 @@ def test_rotation_decrypts_to_rotated_message():
     assert max(abs(int(d) - w) for d, w in zip(dec, want)) < 1 << 20
 
 
+@pytest.mark.parametrize("dnum", [3, 2])
+def test_hoisted_rotations_decrypt_to_rotated_messages(dnum):
+    """pyoracle.rotate_hoisted (one ModUp for several Galois elements): every output decrypts to
+    sigma_k(m) + small noise, like the unhoisted rotate; the outputs are not bit-identical to
+    rotate's (ModUp of sigma c1 vs sigma of ModUp c1) but their decryptions agree up to noise."""
+    log_n, L, K = 5, 3, 2
+    n = 1 << log_n
+    mods = pyoracle.gen_moduli(log_n, L + K)
+    qs, ps = mods[:L], mods[L:]
+    rng = random.Random(33 + dnum)
+    s = [rng.randrange(-1, 2) for _ in range(n)]
+    m = [rng.randrange(-1000, 1000) for _ in range(n)]
+    col = pyoracle._mods_col(qs)
+    s_n = pyoracle.rns_ntt_fwd(pyoracle._to_rns(s, qs), qs)
+    a = np.stack([np.array([rng.randrange(q) for _ in range(n)], dtype=object) for q in qs])
+    e = pyoracle.rns_ntt_fwd(pyoracle._to_rns([rng.randrange(-3, 4) for _ in range(n)], qs), qs)
+    m_n = pyoracle.rns_ntt_fwd(pyoracle._to_rns(m, qs), qs)
+    ct = np.stack([(-a * s_n + e + m_n) % col, a])
+    ks = [pyoracle.galois_elt(r, n) for r in (1, -3, 5)] + [2 * n - 1]
+    keys = [pyoracle.gen_rot_key(s, k, qs, ps, dnum, rng) for k in ks]
+    outs = pyoracle.rotate_hoisted(ct, ks, keys, qs, ps, dnum, log_n)
+    assert outs.shape == (len(ks), 2, L, n)
+    for k, (rb, ra), out in zip(ks, keys, outs):
+        dec = pyoracle.crt_centered(pyoracle.rns_ntt_inv((out[0] + out[1] * s_n) % col, qs), qs)
+        want = pyoracle.automorphism_coeff(np.array([[v % qs[0] for v in m]], dtype=object), k,
+                                           [qs[0]])[0]
+        want = [int(v) - qs[0] if int(v) > qs[0] // 2 else int(v) for v in want]
+        assert max(abs(int(d) - w) for d, w in zip(dec, want)) < 1 << 20
+        ref = pyoracle.rotate(ct, k, rb, ra, qs, ps, dnum, log_n)
+        dref = pyoracle.crt_centered(pyoracle.rns_ntt_inv((ref[0] + ref[1] * s_n) % col, qs), qs)
+        assert max(abs(int(x) - int(y)) for x, y in zip(dec, dref)) < 1 << 20
+
+
 # ---- SURVEY.md §8(f) row 3: Philox and samplers ---------------------------------------------
 
 def test_philox_known_answers():
