@@ -252,7 +252,8 @@ size_t rotate_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch) {
 // the bulk of a key-switch -- runs once, and each rotation reads the NTT-form digits through its
 // automorphism inside the inner product (sigma commutes with the digit decomposition up to the
 // conversion's multiples of the digit modulus, which the key-switch tolerates either way).  Per
-// rotation: sigma(c0), the gathered inner product, ModDown with sigma(c0) added in its finish.
+// rotation: the gathered inner product, then ModDown with sigma(c0) added in its finish (gathered
+// there too on the fused ModDown; a separate sigma(c0) pass on the wide contexts).
 // Restated by oracle/pyoracle.py rotate_hoisted; decrypts to sigma_k(m) like fhe_rotate, but is
 // not bit-identical to it (ModUp of sigma(c1) vs sigma of ModUp(c1)).
 int launch_rotate_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* galois,
@@ -288,15 +289,21 @@ int launch_rotate_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* 
     return rc;
   for (u32 r = 0; r < count; ++r) {
     u64* o = out + (u64)r * batch * 2 * ln;
-    if ((rc = launch_automorphism(c, sc0, ln, in, 2 * ln, batch, 0, L, galois[r], true, s)))
-      return rc;
     KsHoist h;
     h.galois = galois[r];
     h.ydn = ydn;
     KsEpilogue ep;
     ep.out_bs = 2 * ln;
-    ep.add0 = sc0;
-    ep.add_bs = ln;
+    if (ks_hoist_fused_down(c)) {  // the ModDown finish reads c0 through sigma itself
+      ep.add0 = in;
+      ep.add_bs = 2 * ln;
+      ep.add_gal = galois[r];
+    } else {
+      if ((rc = launch_automorphism(c, sc0, ln, in, 2 * ln, batch, 0, L, galois[r], true, s)))
+        return rc;
+      ep.add0 = sc0;
+      ep.add_bs = ln;
+    }
     if ((rc = launch_keyswitch_shard(c, o, o + ln, call, c1, rot_b[r], rot_a[r], 0, L, batch, kws,
                                      s, &ep, &h)))
       return rc;

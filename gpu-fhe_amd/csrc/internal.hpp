@@ -136,10 +136,13 @@ struct KsEpilogue {
   const u64* add0 = nullptr;
   const u64* add1 = nullptr;
   u64 add_bs = 0;
+  u32 add_gal = 0;  // != 0: add rows read through sigma_add_gal's NTT-domain gather (k_moddown_row)
 };
 // Hoisted rotations (galois.hip launch_rotate_hoisted): modup_only runs ModUp alone and leaves the
 // NTT-form digits in the workspace's ext region; otherwise the key-switch skips ModUp and reads
 // those digits (and d2_own) through sigma_galois inside the inner product (unfused kernels).
+// The hoisted rotation's inner step takes the fused ModDown (whose finish can gather sigma(c0))
+inline bool ks_hoist_fused_down(const fhe_ctx* c) { return c->K <= 4 && c->dnum <= 4 && !c->wide; }
 struct KsHoist {
   bool modup_only = false;
   u32 galois = 0;

@@ -1090,9 +1090,24 @@ struct FinishView {
   u32 lane;
   u64 q;
   ulonglong2 pinv;
+  u32 gal = 0;    // != 0: the addend is read through sigma_gal (hoisted rotation: sigma(c0))
+  u32 rbase = 0;  // slot of add[0] within its poly
+  u32 log_n = 0;
+  __device__ __forceinline__ u32 gal_src(u32 i) const {
+    const u32 sh = 32 - log_n;
+    const u32 g = ((2 * (__builtin_bitreverse32(i) >> sh) + 1) * gal) & ((2u << log_n) - 1);
+    return __builtin_bitreverse32((g - 1) >> 1) >> sh;
+  }
   __device__ __forceinline__ u64x2_t plus(u64x2_t r, u32 off) const {
     if (!add) return r;  // kernel-argument uniform
-    const u64x2_t a = *(const __attribute__((address_space(1))) u64x2_t*)(add + off);
+    u64x2_t a;
+    if (gal) {  // kernel-argument uniform; the sources of a row stay inside its aligned block
+      const __attribute__((address_space(1))) u64* base =
+          (const __attribute__((address_space(1))) u64*)(add - rbase);
+      a = u64x2_t{base[gal_src(rbase + off)], base[gal_src(rbase + off + 1)]};
+    } else {
+      a = *(const __attribute__((address_space(1))) u64x2_t*)(add + off);
+    }
     return u64x2_t{csub(r.x + a.x, q), csub(r.y + a.y, q)};
   }
   template <class Lay>
@@ -1155,7 +1170,7 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   const FinishView fo{(h ? ks1 : ks0) + (u64)b * ep.out_bs + (u64)l * N + rloc,
                       acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc,
                       add ? add + (u64)b * ep.add_bs + (u64)l * N + rloc : nullptr, lane, q,
-                      pinv[limb]};
+                      pinv[limb], ep.add_gal, (u32)rloc, (u32)LOGN};
   // column-passed by k_modup_col (inputs below 2q) or k_ntt_col (below q)
   pass_run<G::N2, true, kFinalFwd, kWaveSync, true, H, fwd_range(2, G::N1, H), true>(
       x, fo, lv, t, tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, q, {0, 0}, {0, 0});

@@ -490,7 +490,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   u64* accp = acc + (u64)nlimbs * n;
   // (a hoisted rotation's inner step too, with its own scratch for the INTT output)
   const bool fused_down = K <= 4 && ((fused && (u64)c->dnum * rows >= 2 * (u64)K) ||
-                                     (hoist && hoist->ydn && fusable));
+                                     (hoist && hoist->ydn && ks_hoist_fused_down(c)));
   // Fused ModDown (fused path, K <= 4): the P -> Q conversion runs inside the column-forward
   // pass of the conversion NTT (k_modup_col, as ModUp), on the P rows the INTT has already scaled
   // into the ext region (free once the inner product has run): conv is never written in
