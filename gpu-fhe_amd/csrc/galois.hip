@@ -219,7 +219,10 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
   u64* sc0 = sc1 + batch * ln;
   u64* kws = sc0 + batch * ln;
   int rc;
-  if ((rc = launch_automorphism(c, sc0, ln, in, 2 * ln, batch, 0, L, galois_elt, true, s)) ||
+  // sigma(c0) is gathered by the ModDown finish itself where that is k_moddown_row
+  const bool gather0 = ks_fused(c);
+  if ((!gather0 &&
+       (rc = launch_automorphism(c, sc0, ln, in, 2 * ln, batch, 0, L, galois_elt, true, s))) ||
       (rc = launch_automorphism(c, sc1, ln, in + ln, 2 * ln, batch, 0, L, galois_elt, true, s)))
     return rc;
   // key-switch sigma(c1): its coefficient form goes to the tail of the key-switch workspace
@@ -234,8 +237,9 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
   // out = (sigma(c0) + ks0, ks1) straight out of the key-switch's ModDown finish (KsEpilogue)
   KsEpilogue ep;
   ep.out_bs = 2 * ln;
-  ep.add0 = sc0;
-  ep.add_bs = ln;
+  ep.add0 = gather0 ? in : sc0;
+  ep.add_bs = gather0 ? 2 * ln : ln;
+  ep.add_gal = gather0 ? galois_elt : 0;
   return launch_keyswitch_shard(c, out, out + ln, call, sc1, rot_b, rot_a, 0, L, batch, kws, s,
                                 &ep);
 }

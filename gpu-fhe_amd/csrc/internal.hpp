@@ -141,6 +141,8 @@ struct KsEpilogue {
 // Hoisted rotations (galois.hip launch_rotate_hoisted): modup_only runs ModUp alone and leaves the
 // NTT-form digits in the workspace's ext region; otherwise the key-switch skips ModUp and reads
 // those digits (and d2_own) through sigma_galois inside the inner product (unfused kernels).
+// Whether a key-switch finishes in k_moddown_row (which can gather its addend, add_gal)
+inline bool ks_fused(const fhe_ctx* c) { return c->dnum <= 4 && !c->wide; }
 // The hoisted rotation's inner step takes the fused ModDown (whose finish can gather sigma(c0))
 inline bool ks_hoist_fused_down(const fhe_ctx* c) { return c->K <= 4 && c->dnum <= 4 && !c->wide; }
 struct KsHoist {

@@ -406,8 +406,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   // ranges and 128-bit sums that need q < 2^61.
   // Hoisted rotations (KsHoist) take the unfused kernels: the digits must exist in NTT form in
   // HBM so that each rotation's inner product can gather them through its automorphism.
-  const bool fusable = c->dnum <= 4 && !c->wide;
-  const bool fused = !hoist && fusable;
+  const bool fused = !hoist && ks_fused(c);
   const u32 gal = hoist ? hoist->galois : 0;
   // Fused ModUp (with the fused row kernel, digits of <= 4 limbs): the base conversion runs
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
