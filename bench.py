@@ -59,6 +59,11 @@ def parse():
                          "exact wide-modulus butterflies)")
     ap.add_argument("--ks-chunks", type=int, default=0,
                     help="keyswitch: all-gather chunks per batch (0 = 1 at N = 1, 4 above)")
+    ap.add_argument("--ks-batch", type=int, default=16,
+                    help="keyswitch (and the default line's key-switch leg): ciphertexts per "
+                         "call, the whole job's (limbs sharded: strong scaling)")
+    ap.add_argument("--no-keyswitch-leg", action="store_true",
+                    help="hommult: skip the key-switch ride-along leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -143,7 +148,16 @@ def cpu_model():
 
 
 def cpu_threads():
-    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    """OpenMP threads the baseline runs with: OMP_NUM_THREADS (the GPU box allots 16 host CPUs per
+    GPU and sets it), else every CPU this process may run on."""
+    return int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+
+
+def cpu_host():
+    """What the cpu_baseline ran on: the model, the threads used, the CPUs this process may use
+    (sched_getaffinity) and the machine's total (os.cpu_count: the whole box, shared)."""
+    return {"cpu_model": cpu_model(), "threads": cpu_threads(),
+            "affinity_cpus": len(os.sched_getaffinity(0)), "host_cpus": os.cpu_count()}
 
 
 def cpu_baseline_hommult(moduli, log_n, budget_s):
@@ -168,7 +182,7 @@ def cpu_baseline_hommult(moduli, log_n, budget_s):
         done += B
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 2), "unit": "HomMult/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            **cpu_host(),
             "sample": f"{done} HomMults (N=2^{log_n}, L={L}, batches of {B}) by the tuned C port "
                       f"oracle/fhe_cpu_port.c (bit-exact with the checker), OpenMP {threads} "
                       f"threads, in {dt:.1f} s"}
@@ -177,22 +191,28 @@ def cpu_baseline_hommult(moduli, log_n, budget_s):
 def traffic_from_profile(kernel, shape):
     """HBM bytes per launch of `kernel` from profiles/hbm_traffic.json when it was measured on
     this exact per-GPU shape (FETCH_SIZE/WRITE_SIZE passes, corrected as MI355X_MICROARCH.md
-    §HBM prescribes); otherwise null."""
+    §HBM prescribes); otherwise null.  Returns (bytes, source)."""
+    path = os.path.join("profiles", "hbm_traffic.json")
     try:
-        with open(os.path.join(ROOT, "profiles", "hbm_traffic.json")) as f:
-            rec = json.load(f).get(kernel)
+        with open(os.path.join(ROOT, path)) as f:
+            tab = json.load(f)
     except (OSError, ValueError):
-        return None
-    if not rec or rec.get("shape") != shape:
-        return None
-    return rec.get("bytes_per_launch")
+        return None, None
+    rec = tab.get(kernel)
+    if not rec or rec.get("shape") != shape or rec.get("bytes_per_launch") is None:
+        return None, None
+    return rec["bytes_per_launch"], (f"committed, not measured in this run: {path} = "
+                                     f"{tab.get('_source', 'rocprofv3 PMC passes')}, same kernel "
+                                     "and per-GPU shape")
 
 
 def roofline(kernel, alg_bytes, ms, shape):
     achieved = alg_bytes / (ms * 1e-3) / 1e9
+    traffic, src = traffic_from_profile(kernel, shape)
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profile(kernel, shape),
-            "kernel": kernel, "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(ms, 4)}
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "traffic_source": src, "kernel": kernel, "alg_bytes_per_launch": alg_bytes,
+            "kernel_ms": round(ms, 4)}
 
 
 _PEAKS = {}
@@ -242,6 +262,14 @@ def roofline_alu(kernel, fwd_bflies, inv_bflies, ms, valu_per_bfly=None):
 
 
 def run_hommult(args, world, rank):
+    """The headline line (BASELINE configs[2]) with two ride-along legs that share its process:
+    the NTTs/sec half of the metric (forward + inverse NTTs, N = 2^16, 8 limbs) and the configs[3]
+    key-switch through the native RCCL path (fhe_keyswitch_dist: limbs sharded over the ranks, one
+    all-gather per chunk), so that the driver's 1 -> 8 GPU runs also measure the only collective.
+    Order: everything is allocated first; the NTT leg runs first (it also brings the chip to its
+    sustained clock, which the driver's short --warmup would otherwise leave inside the timed
+    region: DESIGN.md §8 "Warmup matters"), then the HomMult leg (W warmup + exactly K timed
+    steps), then the key-switch leg."""
     L = 8
     shard = fdist.LimbShard(L, world, rank)
     n = 1 << args.log_n
@@ -256,24 +284,25 @@ def run_hommult(args, world, rank):
     d = ctx.empty(gbatch, 3, shard.nlimbs, n)
     ws = ctx.workspace(load().fhe_hommult_workspace(ctx.handle, gbatch, shard.nlimbs))
     step = lambda: fdist.sharded_hommult(ctx, a, b, shard, out=d, workspace=ws)  # noqa: E731
+    # NTT throughput rides along (BASELINE metric "NTTs/sec"): forward + inverse NTTs of 64 polys
+    # on this rank's limbs, sustained (warmed up, then timed like the main leg), every NTT counted
+    x = uniform_limbs(gen, mods, (64,), n)
+    ks = None if args.no_keyswitch_leg or args.bits != 60 else KeyswitchLeg(args, world, rank)
+
+    def ntt_pair():
+        ctx.ntt_(x, limb0=shard.lo)
+        ctx.intt_(x, limb0=shard.lo)
+
+    nargs = argparse.Namespace(warmup=100, steps=200)
+    ntt_dt, ntt_k = timed(ntt_pair, nargs, world, 8 * nargs.steps + 8)
+    ntt_per_s = 2 * 64 * shard.nlimbs * world * nargs.steps / ntt_dt
+
     dt, kavg = timed(step, args, world, 8 * args.steps + 8)
     hm_per_s = gbatch * args.steps / dt  # each rank covers its limbs of all gbatch pairs
     shape = {"log_n": args.log_n, "batch": gbatch, "nlimbs": shard.nlimbs}
     # dominant kernel: reads 4 and writes 3 polynomials of this rank's limbs = algorithmic traffic
     dom = "hm_row_tensor"
     alg = gbatch * 7 * shard.nlimbs * n * 8
-
-    # NTT throughput rides along (BASELINE metric "NTTs/sec"): forward + inverse NTTs of 64 polys
-    # on this rank's limbs, sustained (warmed up, then timed like the main leg), every NTT counted
-    x = uniform_limbs(gen, mods, (64,), n)
-
-    def ntt_pair():
-        ctx.ntt_(x, limb0=shard.lo)
-        ctx.intt_(x, limb0=shard.lo)
-
-    nargs = argparse.Namespace(warmup=50, steps=100)
-    ntt_dt, ntt_k = timed(ntt_pair, nargs, world, 8 * nargs.steps + 8)
-    ntt_per_s = 2 * 64 * shard.nlimbs * world * nargs.steps / ntt_dt
     pipe_gbps = hm_per_s * 7 * L * n * 8 / 1e9 / world
     out = {
         "metric": METRIC, "value": round(hm_per_s, 2), "unit": "HomMult/s",
@@ -284,7 +313,7 @@ def run_hommult(args, world, rank):
         "ntt_per_sec": round(ntt_per_s, 1),
         "ntt_config": {"log_n": args.log_n, "direction": "forward+inverse", "polys": 64,
                        "limbs_per_gpu": shard.nlimbs, "warmup": nargs.warmup,
-                       "steps": nargs.steps},
+                       "steps": nargs.steps, "order": "run before the HomMult leg"},
         "ntt_kernel_ms": {k: round(v, 4) for k, v in ntt_k.items()},
         "hommult_pipeline_hbm_gbps_per_gpu": round(pipe_gbps, 1),
         "hommult_pipeline_frac_of_peak": round(pipe_gbps / HBM_PEAK_GBPS, 4),
@@ -307,6 +336,8 @@ def run_hommult(args, world, rank):
         out["roofline"]["frac"] else "hbm"
     if args.bits != 60:
         out["config"]["modulus_bits"] = args.bits
+    if ks is not None:
+        out["keyswitch_leg"] = ks.run(argparse.Namespace(warmup=20, steps=50))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_hommult(ctx.moduli, args.log_n, args.cpu_seconds)
@@ -356,7 +387,57 @@ def run_vec(args, world, rank):
         out_line["roofline_" + k] = roofline(k, per_op, v, {"log_n": args.log_n, "polys": polys})
     dom = max(kavg, key=kavg.get)
     out_line["roofline"] = roofline(dom, per_op, kavg[dom], {"log_n": args.log_n, "polys": polys})
-    return out_line, None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_vec(ctx.moduli, args.log_n, args.cpu_seconds)
+    return out_line, cpu
+
+
+def cpu_baseline_vec(moduli, log_n, budget_s):
+    """The reference's vec_add / vec_sub / vec_mul (/root/reference/arithmetic.py:3-13) on this
+    host: the tuned C port (oracle/fhe_cpu_port.c port_vec_op: exact, OpenMP over rows, no `%`;
+    bit-exact with the checker, tests/test_oracle.py) over 64 polys x 8 limbs x N, one add + one
+    sub + one mul per step like the GPU leg: coefficient-ops/s.  Beside it, the reference's own
+    numpy expression `(a op b) % MOD` on uint64 (single thread, what arithmetic.py executes; wrong
+    for sub when a < b and for every 60-bit mul), timed on a smaller sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle  # noqa: E402
+
+    rng = np.random.default_rng(5)
+    n, L, P = 1 << log_n, len(moduli), 64
+    a = np.stack([rng.integers(0, q, (P, n), dtype=np.uint64) for q in moduli], axis=1)
+    b = np.stack([rng.integers(0, q, (P, n), dtype=np.uint64) for q in moduli], axis=1)
+    a2, b2 = a.reshape(P * L, n), b.reshape(P * L, n)
+    rowm = np.tile(np.asarray(moduli, dtype=np.uint64), P)
+    out = np.empty_like(a2)
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < budget_s:
+        for op in ("add", "sub", "mul"):
+            coracle.port_vec_op(op, a2, b2, rowm, out=out)
+        done += 3 * a2.size
+    dt = time.perf_counter() - t0
+    # the reference's numpy expression, single-threaded, on 8 polys x 8 limbs
+    qa, qb = a[:8], b[:8]
+    qm = np.asarray(moduli, dtype=np.uint64)[None, :, None]
+    t1 = time.perf_counter()
+    ref_done = 0
+    while time.perf_counter() - t1 < min(2.0, budget_s):
+        np.remainder(np.add(qa, qb), qm)
+        np.remainder(np.subtract(qa, qb), qm)
+        np.remainder(np.multiply(qa, qb), qm)
+        ref_done += 3 * qa.size
+    rdt = time.perf_counter() - t1
+    return {"value": round(done / dt, 1), "unit": "coeff-op/s", "cores": cpu_threads(),
+            "kind": "port", **cpu_host(),
+            "sample": f"{done / 3 / a2.size:.0f} steps of add + sub + mul over {P} polys x {L} limbs "
+                      f"x N=2^{log_n} by the tuned C port (port_vec_op, exact), OpenMP "
+                      f"{cpu_threads()} threads, in {dt:.1f} s",
+            "reference_numpy_uint64": {
+                "value": round(ref_done / rdt, 1), "unit": "coeff-op/s", "cores": 1,
+                "note": "the reference's own expression (a op b) % MOD with numpy uint64 "
+                        "(/root/reference/arithmetic.py:3-13), 8 polys x 8 limbs, "
+                        f"{rdt:.1f} s; inexact for sub (a < b) and 60-bit mul"}}
 
 
 def run_ntt(args, world, rank):
@@ -420,7 +501,7 @@ def cpu_baseline_ntt(moduli, log_n, budget_s):
         done += 2 * P * len(mods)
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 1), "unit": "NTT/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            **cpu_host(),
             "sample": f"{done} forward+inverse NTTs (N=2^{log_n}, {len(mods)} limbs x {P} polys per "
                       f"call) by the tuned C port oracle/fhe_cpu_port.c, OpenMP {threads} threads, "
                       f"in {dt:.1f} s"}
@@ -449,7 +530,7 @@ def cpu_baseline_keyswitch(moduli, special, log_n, dnum, budget_s):
         done += B
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 2), "unit": "keyswitch/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            **cpu_host(),
             "sample": f"{done} key-switches (N=2^{log_n}, L={len(moduli)}, K={len(special)}, "
                       f"dnum={dnum}, batches of {B}) by the tuned C port oracle/fhe_cpu_port.c "
                       f"(bit-exact with the checker), OpenMP {threads} threads, in {dt:.1f} s"}
@@ -495,58 +576,113 @@ def run_ntt_batch(args, world, rank):
     return out, cpu
 
 
+def valu_profile():
+    """profiles/r03_keyswitch_pmc.json: per-kernel SQ_INSTS_VALU per launch of the key-switch at
+    the bench shape (rocprofv3 --pmc pass, tools/valu_roofline.py), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r03_keyswitch_pmc.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+class KeyswitchLeg:
+    """BASELINE configs[3] through the native multi-GPU path: N = 2^16, L = 16, K = 4, dnum = 4,
+    a global batch of `--ks-batch` ciphertexts (one key), limbs sharded over the ranks, INTT +
+    one ncclAllGather per chunk + the local key-switch inside libfhecore (fhe_keyswitch_dist on
+    its own RCCL communicator; one chunk at N = 1, 4 above so transfers overlap compute).  The
+    batch is the whole job's: strong scaling.  Allocates on construction, times in run()."""
+
+    L, K, DNUM = 16, 4, 4
+
+    def __init__(self, args, world, rank):
+        self.world, self.rank = world, rank
+        self.shard = fdist.LimbShard(self.L, world, rank)
+        self.log_n = args.log_n
+        n = 1 << args.log_n
+        self.ctx = ctx = fc.Context(args.log_n, L=self.L, K=self.K, dnum=self.DNUM)
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(7 + rank)
+        rows = self.shard.evk_rows(self.K)
+        allm = ctx.all_moduli
+        self.evk_b = uniform_limbs(gen, [allm[r] for r in rows], (self.DNUM,), n)
+        self.evk_a = uniform_limbs(gen, [allm[r] for r in rows], (self.DNUM,), n)
+        self.B = args.ks_batch
+        self.d2 = uniform_limbs(gen, ctx.moduli[self.shard.lo:self.shard.hi], (self.B,), n)
+        self.comm = fdist.RcclComm()
+        self.chunks = args.ks_chunks or (1 if world == 1 else 4)
+        self.ws = ctx.workspace(load().fhe_keyswitch_dist_workspace(ctx.handle, self.comm.handle,
+                                                                    self.B, self.chunks))
+
+    def step(self):
+        self.ctx.keyswitch_dist(self.comm, self.d2, self.evk_b, self.evk_a, chunks=self.chunks,
+                                workspace=self.ws)
+
+    def run(self, targs):
+        L, K, dnum, B, world = self.L, self.K, self.DNUM, self.B, self.world
+        n = 1 << self.log_n
+        dt, kavg = timed(self.step, targs, world, 64 * targs.steps + 64)
+        gather = self.comm.gather_ms()  # the last call's chunks
+        ks_per_s = B * targs.steps / dt
+        ms_per_ks = dt / (B * targs.steps) * 1e3
+        # SURVEY.md §8d: d2 in + evk (dnum * 2 * (L + K) limbs) + 2 L limbs out per key-switch; the
+        # key is shared by the batch, so per batch: B (d2 + out) + one key, unsharded
+        alg = (B * 3 * L + dnum * 2 * (L + K)) * n * 8 // B
+        res = {"value": round(ks_per_s, 2), "unit": "keyswitch/s",
+               "ms_per_step": round(dt / targs.steps * 1e3, 4),
+               "config": {"workload": "hybrid key-switch, BASELINE configs[3] (fhe_keyswitch_dist)",
+                          "log_n": self.log_n, "L": L, "K": K, "dnum": dnum, "batch": B,
+                          "chunks": self.chunks, "scaling": "strong",
+                          "parallelism": f"rns-limb-shard x{world}, RCCL all-gather"},
+               "warmup": targs.warmup, "steps": targs.steps,
+               "gather_ms_per_chunk": [round(v, 4) for v in gather],
+               "keyswitch_alg_hbm_gbps_per_gpu": round(ks_per_s * alg / 1e9 / world, 1),
+               "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
+               "roofline": roofline("keyswitch (whole, per GPU)", alg // world, ms_per_ks,
+                                    {"log_n": self.log_n, "L": L, "world": world})}
+        plan = fdist.dist_plan(L, self.log_n, world, self.rank, B, self.chunks)
+        res["gather_bytes_per_chunk"] = plan.block_words * 8 * world  # what each rank ends up with
+        # integer-ALU roofline of one key-switch on this rank, butterflies only: INTT of the own
+        # d2 limbs; ModUp: every digit's extended rows = dnum (nl + K) - nl forward NTTs; ModDown:
+        # INTT of the 2 K special rows, forward NTT of the 2 nl converted rows
+        nl, full = self.shard.nlimbs, (n // 2) * self.log_n
+        res["roofline_alu"] = roofline_alu(
+            "keyswitch (whole, per GPU; NTT butterflies only)",
+            (dnum * (nl + K) + nl) * full, (nl + 2 * K) * full, ms_per_ks)
+        # ... and by VALU instruction issue, which counts everything the kernels execute (base
+        # conversion products, inner products, reductions, addressing): SQ_INSTS_VALU per launch
+        # of each key-switch kernel at this shape (committed rocprofv3 --pmc pass) over this run's
+        # time, against the issue rate of the butterfly ceiling kernel in that profiled process
+        prof = valu_profile()
+        if prof and world == 1 and B == prof.get("shape", {}).get("batch"):
+            per_step = sum(v["valu_instr_per_launch"] * v["launches_per_step"]
+                           for k, v in prof["kernels"].items() if k.startswith("k_") and
+                           "bfly_peak" not in k)
+            ach = per_step / (dt / targs.steps) / 1e9
+            res["roofline_valu"] = {
+                "bound": "valu", "achieved": round(ach, 1), "peak": prof["ceiling_valu_g_per_s"],
+                "unit": "G VALU wave-instructions/s", "frac": round(ach / prof["ceiling_valu_g_per_s"], 4),
+                "valu_instr_per_step": per_step,
+                "valu_source": "committed, not measured in this run: profiles/r03_keyswitch_pmc.json "
+                               "(SQ_INSTS_VALU of every key-switch kernel, same shape); time from this run",
+                "per_kernel_frac_of_peak": {k: v.get("frac_of_bfly_peak_issue")
+                                            for k, v in prof["kernels"].items()
+                                            if k.startswith("k_") and "bfly_peak" not in k}}
+        return res
+
+
 def run_keyswitch(args, world, rank):
-    L, K, dnum = 16, 4, 4
-    shard = fdist.LimbShard(L, world, rank)
-    n = 1 << args.log_n
-    ctx = fc.Context(args.log_n, L=L, K=K, dnum=dnum)
-    gen = torch.Generator(device="cuda")
-    gen.manual_seed(7 + rank)
-    rows = shard.evk_rows(K)
-    allm = ctx.all_moduli
-    evk_b = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
-    evk_a = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
-    B = args.batch
-    d2 = uniform_limbs(gen, ctx.moduli[shard.lo:shard.hi], (B,), n)
-    # the native path: libfhecore's RCCL communicator, INTT + all-gather + key-switch in
-    # fhe_keyswitch_dist, chunked so a chunk's transfer overlaps the previous chunk's work (one
-    # chunk at N = 1: nothing to overlap, and a whole batch reads the key once)
-    comm = fdist.RcclComm()
-    chunks = args.ks_chunks or (1 if world == 1 else 4)
-    ws = ctx.workspace(load().fhe_keyswitch_dist_workspace(ctx.handle, comm.handle, B, chunks))
-
-    def step():
-        ctx.keyswitch_dist(comm, d2, evk_b, evk_a, chunks=chunks, workspace=ws)
-
-    dt, kavg = timed(step, args, world, 64 * args.steps + 64)
-    ks_per_s = B * args.steps / dt
-    # d2 in + evk (dnum * 2 * (L + K) limbs) + 2 L limbs out per key-switch; the
-    # key is shared by the batch, so per batch: B (d2 + out) + one key, unsharded
-    alg = (B * 3 * L + dnum * 2 * (L + K)) * n * 8 // B
-    gbps = ks_per_s * alg / 1e9 / world
-    dom = max(kavg, key=kavg.get)
-    out = {"metric": "key-switches/sec at N=2^16, L=16, K=4, dnum=4 (RNS limbs sharded, RCCL all-gather)",
-           "value": round(ks_per_s, 2), "unit": "keyswitch/s",
-           "ms_per_step": round(dt / args.steps * 1e3, 4),
-           "config": {"workload": "hybrid key-switch, BASELINE configs[3] (fhe_keyswitch_dist)",
-                      "log_n": args.log_n, "L": L, "K": K, "dnum": dnum, "batch": B,
-                      "chunks": chunks, "parallelism": f"rns-limb-shard x{world}"},
-           "keyswitch_alg_hbm_gbps_per_gpu": round(gbps, 1),
-           "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
-           "roofline": roofline("keyswitch (whole, per GPU)", alg // world, dt / (B * args.steps) * 1e3,
-                                {"log_n": args.log_n, "L": L, "world": world})}
-    # integer-ALU roofline of one key-switch on this rank: its NTT butterflies (INTT of the own d2
-    # limbs; ModUp: every digit's extended rows = dnum (nl + K) - nl forward NTTs; ModDown: INTT of
-    # the 2 K special rows, forward NTT of the 2 nl converted rows) against the butterfly ceiling.
-    # The base conversions (ModUp dnum x 4 x (nl + K) products per coefficient, ModDown 2 K x nl)
-    # are extra VALU work the ceiling does not count, so this fraction understates the kernels.
-    nl, full = shard.nlimbs, (n // 2) * args.log_n
-    out["roofline_alu"] = roofline_alu(
-        "keyswitch (whole, per GPU; NTT butterflies only, base conversions not counted)",
-        (dnum * (nl + K) + nl) * full, (nl + 2 * K) * full, dt / (B * args.steps) * 1e3)
+    leg = KeyswitchLeg(args, world, rank)
+    out = leg.run(args)
+    out["metric"] = ("key-switches/sec at N=2^16, L=16, K=4, dnum=4 (RNS limbs sharded, RCCL "
+                     "all-gather)")
+    out.pop("warmup")
+    out.pop("steps")
+    out["scaling"] = out["config"].pop("scaling")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_keyswitch(ctx.moduli, ctx.special, args.log_n, dnum, args.cpu_seconds)
+        cpu = cpu_baseline_keyswitch(leg.ctx.moduli, leg.ctx.special, args.log_n, leg.DNUM,
+                                     args.cpu_seconds)
     return out, cpu
 
 
@@ -585,7 +721,55 @@ def run_mulrelin(args, world, rank):
                            "parallelism": f"replicas x{world}"},
                 "roofline": roofline("mul_relin (whole pipeline)", alg, dt / (B * args.steps) * 1e3 * world,
                                      {"log_n": args.log_n, "L": L})}
-    return out_line, None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_mulrelin(ctx.moduli, ctx.special, args.log_n, dnum, args.cpu_seconds)
+    return out_line, cpu
+
+
+def cpu_baseline_mulrelin(moduli, special, log_n, dnum, budget_s):
+    """mult + relinearise on this host from the tuned C port's pieces (oracle/fhe_cpu_port.c):
+    the NTT-form tensor by port_vec_op (d0 = a0 b0, d1 = a0 b1 + a1 b0, d2 = a1 b1), the
+    key-switch of d2 by port_keyswitch, the combine by port_vec_op adds.  The rescale the GPU
+    pipeline also runs is NOT included (one INTT + L - 1 NTTs + elementwise per ciphertext
+    polynomial), so this baseline is lighter than the GPU leg."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle  # noqa: E402
+
+    rng = np.random.default_rng(11)
+    n, L = 1 << log_n, len(moduli)
+    allm = list(moduli) + list(special)
+    B = 2
+    ct = [np.stack([rng.integers(0, q, (B, n), dtype=np.uint64) for q in moduli], axis=1)
+          for _ in range(4)]  # a0, a1, b0, b1 [B][L][N]
+    evk = [np.stack([rng.integers(0, q, (dnum, n), dtype=np.uint64) for q in allm], axis=1)
+           for _ in range(2)]
+    rowm = np.tile(np.asarray(moduli, dtype=np.uint64), B)
+    flat = lambda x: x.reshape(B * L, n)  # noqa: E731
+
+    def one():
+        a0, a1, b0, b1 = (flat(x) for x in ct)
+        d0 = coracle.port_vec_op("mul", a0, b0, rowm)
+        d1 = coracle.port_vec_op("add", coracle.port_vec_op("mul", a0, b1, rowm),
+                                 coracle.port_vec_op("mul", a1, b0, rowm), rowm)
+        d2 = coracle.port_vec_op("mul", a1, b1, rowm).reshape(B, L, n)
+        k0, k1 = coracle.port_keyswitch(d2, evk[0], evk[1], moduli, special, dnum)
+        coracle.port_vec_op("add", d0, flat(k0), rowm)
+        coracle.port_vec_op("add", d1, flat(k1), rowm)
+
+    one()  # tables
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < budget_s:
+        one()
+        done += B
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 2), "unit": "mul_relin/s", "cores": cpu_threads(),
+            "kind": "port", **cpu_host(),
+            "sample": f"{done} mult + relinearise (N=2^{log_n}, L={L}, K={len(special)}, "
+                      f"dnum={dnum}, batches of {B}; rescale not included) composed from the tuned "
+                      f"C port (port_vec_op, port_keyswitch), OpenMP {cpu_threads()} threads, "
+                      f"in {dt:.1f} s"}
 
 
 def run_rotate(args, world, rank):
@@ -624,7 +808,62 @@ def run_rotate(args, world, rank):
                        "parallelism": f"replicas x{world}"},
             "unhoisted_rotations_per_sec": round(B * R * args.steps * world / dt_plain, 2),
             "hoisting_speedup": round(dt_plain / dt, 3),
-            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()}}, None
+            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
+            # per rotation: read the ct (2 L limbs), write the rotated ct (2 L), each element's key
+            # (dnum * 2 * (L + K) limbs) once per batch -- algorithmic, as SURVEY §8d counts the
+            # key-switch; the dominant kernel is the gathered inner product (k_ks_inner)
+            "roofline": roofline("hoisted rotation (whole, per GPU)",
+                                 (B * 4 * L + dnum * 2 * (L + K)) * n * 8 // B,
+                                 dt / (B * R * args.steps) * 1e3,
+                                 {"log_n": args.log_n, "L": L, "R": R}),
+            "roofline_inner_product": roofline(
+                "ks_inner (gathered inner product, per launch)",
+                (dnum * B * (L + K) + 2 * dnum * (L + K) + 2 * B * (L + K)) * n * 8,
+                kavg.get("ks_inner", float("nan")), {"log_n": args.log_n, "L": L, "B": B})}, (
+        cpu_baseline_rotate(ctx.moduli, ctx.special, args.log_n, dnum, args.cpu_seconds)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline else None)
+
+
+def cpu_baseline_rotate(moduli, special, log_n, dnum, budget_s):
+    """Rotations on this host: sigma_k of both ciphertext polys (an NTT-domain slot permutation,
+    numpy fancy indexing) + the tuned port's key-switch of sigma(c1) (port_keyswitch) + the
+    combine (port_vec_op) -- unhoisted, one key-switch per rotation, as a CPU library runs it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle  # noqa: E402
+
+    rng = np.random.default_rng(13)
+    n, L = 1 << log_n, len(moduli)
+    allm = list(moduli) + list(special)
+    B = 2
+    c0 = np.stack([rng.integers(0, q, (B, n), dtype=np.uint64) for q in moduli], axis=1)
+    c1 = np.stack([rng.integers(0, q, (B, n), dtype=np.uint64) for q in moduli], axis=1)
+    evk = [np.stack([rng.integers(0, q, (dnum, n), dtype=np.uint64) for q in allm], axis=1)
+           for _ in range(2)]
+    k = pow(5, 1, 2 * n)
+    # NTT-domain automorphism: slot i <- brv(((2 brv(i) + 1) k mod 2N - 1) / 2)
+    idx = np.arange(n)
+    brv = np.array([int(f"{i:0{log_n}b}"[::-1], 2) for i in range(n)])
+    perm = brv[(((2 * brv[idx] + 1) * k) % (2 * n) - 1) // 2]
+    rowm = np.tile(np.asarray(moduli, dtype=np.uint64), B)
+
+    def one():
+        s0 = np.ascontiguousarray(c0[..., perm])
+        s1 = np.ascontiguousarray(c1[..., perm])
+        k0, _ = coracle.port_keyswitch(s1, evk[0], evk[1], moduli, special, dnum)
+        coracle.port_vec_op("add", s0.reshape(B * L, n), k0.reshape(B * L, n), rowm)
+
+    one()
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < budget_s:
+        one()
+        done += B
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 2), "unit": "rotations/s", "cores": cpu_threads(),
+            "kind": "port", **cpu_host(),
+            "sample": f"{done} rotations (N=2^{log_n}, L={L}, K={len(special)}, dnum={dnum}, "
+                      f"batches of {B}, unhoisted) by numpy permutations + the tuned C port's "
+                      f"key-switch, OpenMP {cpu_threads()} threads, in {dt:.1f} s"}
 
 
 def main():
@@ -634,6 +873,8 @@ def main():
     json_fd = os.dup(1)
     os.dup2(2, 1)
     args = parse()
+    if args.workload == "keyswitch" and args.batch is not None:
+        args.ks_batch = args.batch
     if args.batch is None:
         args.batch = 64 if args.workload == "hommult" else 16
     world, rank = dist_setup(args)

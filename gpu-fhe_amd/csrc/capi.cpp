@@ -325,6 +325,11 @@ int fhe_rotate_hoisted(const fhe_ctx* c, uint64_t* out, const uint64_t* in,
     set_error("fhe_rotate_hoisted: null Galois element or key array");
     return kInvalid;
   }
+  for (uint32_t r = 0; r < count; ++r)
+    if (!rot_b[r] || !rot_a[r]) {  // the kernels would dereference it on the device
+      set_error("fhe_rotate_hoisted: null key pointer for rotation " + std::to_string(r));
+      return kInvalid;
+    }
   const uint64_t span = (uint64_t)count * batch * 2 * c->L * c->n;
   if (span && in < out + span && out < in + (uint64_t)batch * 2 * c->L * c->n) {
     set_error("fhe_rotate_hoisted: out must not overlap in");

@@ -11,6 +11,9 @@
 // stream, each chunk's all-gather runs on the communicator's own stream as soon as its INTT is
 // done, and the caller's stream waits for a chunk's gather only right before its key-switch, so
 // chunk k + 1's transfer overlaps chunk k's key-switch.
+// Every offset comes from one host-side plan (fhe_dist_plan_*, exported so that the CPU suite
+// checks it for G = 1..8 without a GPU), and fhe_keyswitch_dist_loopback runs the same plan and
+// the same per-chunk steps for G virtual ranks on one device (the GPU suite's G > 1 path).
 // The reference has no communication code at all (/root/reference/arithmetic.py:1 is its only
 // import); the sharded algorithm is restated by oracle/pyoracle.py keyswitch_shard.
 #include <rccl/rccl.h>
@@ -18,6 +21,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/fhecore.h"
 #include "internal.hpp"
@@ -28,6 +32,9 @@ struct fhe_comm_s {
   hipStream_t stream = nullptr;  // the all-gathers
   static constexpr int kMaxChunks = 16;
   hipEvent_t ev_intt[kMaxChunks] = {}, ev_gather[kMaxChunks] = {};
+  // timing events around each chunk's all-gather on `stream` (fhe_comm_gather_ms)
+  hipEvent_t ev_g0[kMaxChunks] = {}, ev_g1[kMaxChunks] = {};
+  uint32_t last_chunks = 0;
 };
 
 namespace fhe {
@@ -42,6 +49,8 @@ namespace {
     }                                                                                     \
   } while (0)
 
+constexpr uint64_t kBad = ~0ull;
+
 u32 shard_width(u32 L, u32 G) { return (L + G - 1) / G; }
 
 void shard_of(u32 L, u32 G, u32 r, u32* limb0, u32* nlimbs) {
@@ -51,12 +60,45 @@ void shard_of(u32 L, u32 G, u32 r, u32* limb0, u32* nlimbs) {
   *nlimbs = std::min(L, lo + c) - lo;
 }
 
-// Split a batch into nc chunks of cb ciphertexts (the last one possibly shorter, none empty).
-void chunking(u32 batch, u32 chunks, u32* nc, u32* cb) {
-  const u32 want = std::max(1u, std::min({chunks ? chunks : 4u, std::max(batch, 1u),
-                                           (u32)fhe_comm_s::kMaxChunks}));
-  *cb = (std::max(batch, 1u) + want - 1) / want;
-  *nc = (std::max(batch, 1u) + *cb - 1) / *cb;
+// The chunk's view of the gather region: CAll::ranked over one chunk's [G][cb][c][N] blocks --
+// the addressing launch_keyswitch_shard's kernels use for the source rows.
+CAll chunk_call(const fhe_dist_plan& p, const u64* gather, u32 k) {
+  return CAll::ranked(gather + (u64)k * p.ranks * p.block_words, p.L, p.ranks, p.chunk_batch,
+                      1ull << p.log_n);
+}
+
+// One chunk's INTT of this rank's own limbs into its send block (what ncclAllGather sends).
+int dist_intt_chunk(const fhe_ctx* ctx, const fhe_dist_plan& p, u32 k, const u64* d2_own,
+                    u64* gather, hipStream_t s) {
+  u32 b0, bn;
+  fhe_dist_plan_chunk(&p, k, &b0, &bn);
+  if (!p.nlimbs || !bn) return kOk;
+  const u64 n = ctx->n;
+  // the gathered d2 is the prepared ModUp input when the fused ModUp applies: each rank's INTT
+  // folds (D^_k)^-1 of its limbs' digits into its last stage
+  const bool prep = ks_prepared(ctx);
+  return launch_ntt_strided(ctx, false, d2_own + (u64)b0 * p.nlimbs * n, (u64)p.nlimbs * n,
+                            gather + fhe_dist_plan_send_word(&p, b0, 0), (u64)p.width * n, bn,
+                            p.limb0, p.nlimbs, s, prep ? ctx->d_nfold_up : nullptr,
+                            prep && ks_split30(ctx));
+}
+
+// One chunk's local key-switch once its gather has landed.
+int dist_ks_chunk(const fhe_ctx* ctx, const fhe_dist_plan& p, u32 k, u64* ks0, u64* ks1,
+                  const u64* d2_own, const u64* evk_b, const u64* evk_a, const u64* gather,
+                  void* kws, hipStream_t s) {
+  u32 b0, bn;
+  fhe_dist_plan_chunk(&p, k, &b0, &bn);
+  if (!p.nlimbs || !bn) return kOk;
+  CAll call = chunk_call(p, gather, k);
+  call.scaled = ks_prepared(ctx);
+  const u64 off = (u64)b0 * p.nlimbs * ctx->n;
+  return launch_keyswitch_shard(ctx, ks0 + off, ks1 + off, call, d2_own + off, evk_b, evk_a,
+                                p.limb0, p.nlimbs, bn, kws, s);
+}
+
+size_t dist_workspace(const fhe_ctx* ctx, const fhe_dist_plan& p, u32 max_nlimbs) {
+  return p.gather_words * sizeof(u64) + keyswitch_workspace_bytes(ctx, max_nlimbs, p.chunk_batch);
 }
 
 }  // namespace
@@ -65,6 +107,56 @@ void chunking(u32 batch, u32 chunks, u32* nc, u32* cb) {
 using namespace fhe;
 
 extern "C" {
+
+int fhe_dist_plan_make(fhe_dist_plan* p, uint32_t L, uint32_t log_n, uint32_t G, uint32_t r,
+                       uint32_t batch, uint32_t chunks) {
+  if (!p || L == 0 || G == 0 || r >= G || log_n > 30) {
+    set_error("fhe_dist_plan_make: need L >= 1, 0 <= rank < ranks");
+    return kInvalid;
+  }
+  *p = fhe_dist_plan{};
+  p->L = L;
+  p->log_n = log_n;
+  p->ranks = G;
+  p->rank = r;
+  p->batch = batch;
+  shard_of(L, G, r, &p->limb0, &p->nlimbs);
+  p->width = shard_width(L, G);
+  // nc chunks of cb ciphertexts (the last one possibly shorter, none empty); 0 = default 4
+  const u32 b = std::max(batch, 1u);
+  const u32 want = std::max(1u, std::min({chunks ? chunks : 4u, b, (u32)fhe_comm_s::kMaxChunks}));
+  p->chunk_batch = (b + want - 1) / want;
+  p->chunks = (b + p->chunk_batch - 1) / p->chunk_batch;
+  p->block_words = (u64)p->chunk_batch * p->width << log_n;
+  p->gather_words = (u64)p->chunks * G * p->block_words;
+  return kOk;
+}
+
+int fhe_dist_plan_chunk(const fhe_dist_plan* p, uint32_t k, uint32_t* b0, uint32_t* bn) {
+  if (!p || !b0 || !bn || k >= p->chunks) {
+    set_error("fhe_dist_plan_chunk: chunk out of range");
+    return kInvalid;
+  }
+  *b0 = std::min(p->batch, k * p->chunk_batch);
+  *bn = std::min(p->batch, *b0 + p->chunk_batch) - *b0;
+  return kOk;
+}
+
+uint64_t fhe_dist_plan_send_word(const fhe_dist_plan* p, uint32_t b, uint32_t j) {
+  if (!p || b >= p->batch || j >= p->nlimbs) return kBad;
+  const u32 k = b / p->chunk_batch, bi = b % p->chunk_batch;
+  const u64 n = 1ull << p->log_n;
+  // the INTT of chunk k writes this rank's rows at poly stride width N into its block
+  return ((u64)k * p->ranks + p->rank) * p->block_words + ((u64)bi * p->width + j) * n;
+}
+
+uint64_t fhe_dist_plan_read_word(const fhe_dist_plan* p, uint32_t b, uint32_t l) {
+  if (!p || b >= p->batch || l >= p->L) return kBad;
+  const u32 k = b / p->chunk_batch, bi = b % p->chunk_batch;
+  // exactly the kernels' addressing: chunk k's CAll::ranked view, ciphertext bi, limb l
+  const CAll call = CAll::ranked(nullptr, p->L, p->ranks, p->chunk_batch, 1ull << p->log_n);
+  return (u64)k * p->ranks * p->block_words + (u64)bi * call.bs + call.off(l, 1ull << p->log_n);
+}
 
 int fhe_comm_get_unique_id(uint8_t* id) {
   if (!id) {
@@ -101,6 +193,8 @@ int fhe_comm_create(fhe_comm_t* comm, const uint8_t* id, int nranks, int rank, i
   for (int k = 0; k < fhe_comm_s::kMaxChunks && e == hipSuccess; ++k) {
     e = hipEventCreateWithFlags(&c->ev_intt[k], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_gather[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_g0[k]);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_g1[k]);
   }
   if (e != hipSuccess) {
     set_error(std::string("fhe_comm_create: ") + hipGetErrorString(e));
@@ -116,8 +210,8 @@ int fhe_comm_destroy(fhe_comm_t c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (int k = 0; k < fhe_comm_s::kMaxChunks; ++k) {
-    if (c->ev_intt[k]) (void)hipEventDestroy(c->ev_intt[k]);
-    if (c->ev_gather[k]) (void)hipEventDestroy(c->ev_gather[k]);
+    for (hipEvent_t ev : {c->ev_intt[k], c->ev_gather[k], c->ev_g0[k], c->ev_g1[k]})
+      if (ev) (void)hipEventDestroy(ev);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->nccl) (void)ncclCommDestroy(c->nccl);
@@ -134,16 +228,27 @@ int fhe_comm_shard(const fhe_ctx* ctx, fhe_comm_t comm, uint32_t* limb0, uint32_
   return kOk;
 }
 
+int fhe_comm_gather_ms(fhe_comm_t comm, float* ms, uint32_t cap, uint32_t* count) {
+  if (!comm || !count || (cap && !ms)) {
+    set_error("fhe_comm_gather_ms: null argument");
+    return kInvalid;
+  }
+  *count = comm->last_chunks;
+  for (u32 k = 0; k < std::min(cap, comm->last_chunks); ++k) {
+    FHE_HIP_CHECK(hipEventSynchronize(comm->ev_g1[k]));
+    FHE_HIP_CHECK(hipEventElapsedTime(&ms[k], comm->ev_g0[k], comm->ev_g1[k]));
+  }
+  return kOk;
+}
+
 size_t fhe_keyswitch_dist_workspace(const fhe_ctx* ctx, fhe_comm_t comm, uint32_t batch,
                                     uint32_t chunks) {
   if (!ctx || !comm) return 0;
-  u32 limb0, nl;
-  shard_of(ctx->L, (u32)comm->nranks, (u32)comm->rank, &limb0, &nl);
-  const u32 cw = shard_width(ctx->L, (u32)comm->nranks);
-  u32 nc, cb;
-  chunking(batch, chunks, &nc, &cb);
-  const size_t gather = (size_t)nc * comm->nranks * cb * cw * ctx->n * sizeof(u64);
-  return gather + keyswitch_workspace_bytes(ctx, nl, cb);
+  fhe_dist_plan p;
+  if (fhe_dist_plan_make(&p, ctx->L, ctx->log_n, (u32)comm->nranks, (u32)comm->rank, batch,
+                         chunks))
+    return 0;
+  return dist_workspace(ctx, p, p.nlimbs);
 }
 
 int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint64_t* ks1,
@@ -157,52 +262,93 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
     set_error("fhe_keyswitch_dist: context has no special primes (K = 0)");
     return kInvalid;
   }
+  if (comm->device != ctx->device) {
+    // the gathers and their events would run on one device, the kernels on another
+    set_error("fhe_keyswitch_dist: communicator on device " + std::to_string(comm->device) +
+              ", context on device " + std::to_string(ctx->device));
+    return kInvalid;
+  }
+  comm->last_chunks = 0;
   if (batch == 0) return kOk;
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  const u32 G = (u32)comm->nranks, r = (u32)comm->rank, L = ctx->L;
-  u32 limb0, nl;
-  shard_of(L, G, r, &limb0, &nl);
-  const u32 cw = shard_width(L, G);
-  u32 nc, cb;
-  chunking(batch, chunks, &nc, &cb);
-  const u64 n = ctx->n, blk = (u64)cb * cw * n;  // one rank's block of one chunk
+  fhe_dist_plan p;
   int rc;
-  if ((rc = ensure_ws(ctx, fhe_keyswitch_dist_workspace(ctx, comm, batch, chunks), &ws, s)))
+  if ((rc = fhe_dist_plan_make(&p, ctx->L, ctx->log_n, (u32)comm->nranks, (u32)comm->rank, batch,
+                               chunks)))
     return rc;
+  if ((rc = ensure_ws(ctx, dist_workspace(ctx, p, p.nlimbs), &ws, s))) return rc;
   u64* gather = static_cast<u64*>(ws);  // [nc][G][cb][cw][N]
-  // the gathered d2 is the prepared ModUp input when the fused ModUp applies: each rank's INTT
-  // folds (D^_k)^-1 of its limbs' digits into its last stage
-  const bool prep = ks_prepared(ctx);
-  void* kws = gather + (u64)nc * G * blk;
+  void* kws = gather + p.gather_words;
   // 1 + 2: every chunk's INTT into its send block, then its gather on the comm stream
-  for (u32 k = 0; k < nc; ++k) {
-    const u32 b0 = k * cb, bn = std::min(batch, b0 + cb) - b0;
-    u64* gbuf = gather + (u64)k * G * blk;
-    if (nl && bn &&
-        (rc = launch_ntt_strided(ctx, false, d2_own + (u64)b0 * nl * n, (u64)nl * n,
-                                 gbuf + (u64)r * blk, (u64)cw * n, bn, limb0, nl, s,
-                                 prep ? ctx->d_nfold_up : nullptr,
-                                 prep && ks_split30(ctx))))
-      return rc;
+  for (u32 k = 0; k < p.chunks; ++k) {
+    if ((rc = dist_intt_chunk(ctx, p, k, d2_own, gather, s))) return rc;
+    u64* gbuf = gather + (u64)k * p.ranks * p.block_words;
     FHE_HIP_CHECK(hipEventRecord(comm->ev_intt[k], s));
     FHE_HIP_CHECK(hipStreamWaitEvent(comm->stream, comm->ev_intt[k], 0));
-    FHE_NCCL_CHECK(ncclAllGather(gbuf + (u64)r * blk, gbuf, blk, ncclUint64, comm->nccl,
-                                 comm->stream));
+    FHE_HIP_CHECK(hipEventRecord(comm->ev_g0[k], comm->stream));
+    FHE_NCCL_CHECK(ncclAllGather(gbuf + (u64)p.rank * p.block_words, gbuf, p.block_words,
+                                 ncclUint64, comm->nccl, comm->stream));
+    FHE_HIP_CHECK(hipEventRecord(comm->ev_g1[k], comm->stream));
     FHE_HIP_CHECK(hipEventRecord(comm->ev_gather[k], comm->stream));
   }
+  comm->last_chunks = p.chunks;
   prof_mark(s, "ks_dist_intt");
   // 3: each chunk's key-switch once its gather has landed
-  for (u32 k = 0; k < nc; ++k) {
-    const u32 b0 = k * cb, bn = std::min(batch, b0 + cb) - b0;
+  for (u32 k = 0; k < p.chunks; ++k) {
     FHE_HIP_CHECK(hipStreamWaitEvent(s, comm->ev_gather[k], 0));
-    if (!nl || !bn) continue;
-    CAll call = CAll::ranked(gather + (u64)k * G * blk, L, G, cb, n);
-    call.scaled = prep;
-    const u64 off = (u64)b0 * nl * n;
-    if ((rc = launch_keyswitch_shard(ctx, ks0 + off, ks1 + off, call, d2_own + off, evk_b, evk_a,
-                                     limb0, nl, bn, kws, s)))
+    if ((rc = dist_ks_chunk(ctx, p, k, ks0, ks1, d2_own, evk_b, evk_a, gather, kws, s)))
       return rc;
   }
+  return kOk;
+}
+
+size_t fhe_keyswitch_dist_loopback_workspace(const fhe_ctx* ctx, uint32_t ranks, uint32_t batch,
+                                             uint32_t chunks) {
+  if (!ctx || ranks == 0) return 0;
+  fhe_dist_plan p;
+  if (fhe_dist_plan_make(&p, ctx->L, ctx->log_n, ranks, 0, batch, chunks)) return 0;
+  return dist_workspace(ctx, p, p.width);  // rank 0 owns a full block of width limbs
+}
+
+int fhe_keyswitch_dist_loopback(const fhe_ctx* ctx, uint32_t ranks, uint64_t* const* ks0,
+                                uint64_t* const* ks1, const uint64_t* const* d2_own,
+                                const uint64_t* const* evk_b, const uint64_t* const* evk_a,
+                                uint32_t batch, uint32_t chunks, void* ws, fhe_stream_t stream) {
+  if (!ctx || ranks == 0 || !ks0 || !ks1 || !d2_own || !evk_b || !evk_a) {
+    set_error("fhe_keyswitch_dist_loopback: null context or per-rank array, or zero ranks");
+    return kInvalid;
+  }
+  if (ctx->K == 0) {
+    set_error("fhe_keyswitch_dist_loopback: context has no special primes (K = 0)");
+    return kInvalid;
+  }
+  if (batch == 0) return kOk;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  std::vector<fhe_dist_plan> plan(ranks);
+  int rc;
+  for (u32 r = 0; r < ranks; ++r) {
+    if ((rc = fhe_dist_plan_make(&plan[r], ctx->L, ctx->log_n, ranks, r, batch, chunks)))
+      return rc;
+    if (plan[r].nlimbs && (!ks0[r] || !ks1[r] || !d2_own[r] || !evk_b[r] || !evk_a[r])) {
+      set_error("fhe_keyswitch_dist_loopback: null pointer for rank " + std::to_string(r));
+      return kInvalid;
+    }
+  }
+  if ((rc = ensure_ws(ctx, fhe_keyswitch_dist_loopback_workspace(ctx, ranks, batch, chunks), &ws,
+                      s)))
+    return rc;
+  u64* gather = static_cast<u64*>(ws);  // one region shared by the virtual ranks
+  void* kws = gather + plan[0].gather_words;
+  // every rank's INTT writes its own blocks: the region then holds what an in-place all-gather
+  // leaves on each rank
+  for (u32 k = 0; k < plan[0].chunks; ++k)
+    for (u32 r = 0; r < ranks; ++r)
+      if ((rc = dist_intt_chunk(ctx, plan[r], k, d2_own[r], gather, s))) return rc;
+  for (u32 k = 0; k < plan[0].chunks; ++k)
+    for (u32 r = 0; r < ranks; ++r)
+      if ((rc = dist_ks_chunk(ctx, plan[r], k, ks0[r], ks1[r], d2_own[r], evk_b[r], evk_a[r],
+                              gather, kws, s)))
+        return rc;
   return kOk;
 }
 

@@ -147,6 +147,7 @@ int launch_automorphism(const fhe_ctx* c, u64* out, u64 pout, const u64* in, u64
   // coefficient form gathers through k^-1 mod 2N (odd elements form a group mod 2^(logN+1))
   u32 k = galois_elt;
   if (!ntt) k = (u32)modinv_odd_pow2(galois_elt, c->log_n + 1);
+  if (int rc = check_grid(c->n / kThreads, kThreads, nlimbs, polys, "automorphism")) return rc;
   const dim3 g((u32)(c->n / kThreads), nlimbs, polys);
   k_automorph<<<g, kThreads, 0, s>>>(out, pout, in, pin, nlimbs, limb0, c->log_n, k, ntt ? 1 : 0,
                                      c->d_mods);
@@ -168,6 +169,7 @@ int launch_rescale(const fhe_ctx* c, u64* out, const u64* in, u32 polys, u32 nl,
   const u64 n = c->n;
   const ulonglong2* tab = c->d_rs_tab + (size_t)(nl - 1) * c->L;
   const u64* half = c->d_rs_half + (size_t)(nl - 1) * c->L;
+  if (int rc = check_grid(n / kThreads, kThreads, nl - 1, polys, "rescale")) return rc;
   const dim3 g((u32)(n / kThreads), nl - 1, polys);
   if (!ntt) {
     k_rescale_coeff<<<g, kThreads, 0, s>>>(out, in, nl, c->log_n, tab, half, c->d_mods);

@@ -25,6 +25,24 @@ void set_error(const std::string& msg);
 // Records a timing mark after a launch when fhe_prof_begin() is active (prof.cpp).
 void prof_mark(hipStream_t s, const char* name);
 
+// Launch-size guard, called by every launcher before its first launch: the dispatch packet
+// counts work-items along x in 32 bits, and y / z hold at most 65535 workgroups; the launchers
+// narrow their grids to u32, so a size beyond either is refused (FHE_EINVAL) here rather than
+// silently truncated.  (At these kernels' 16 elements per work-item, x overflows only past 2^36
+// residues, more than HBM holds; y / z carry batch / poly counts, reachable at small N.)
+constexpr uint64_t kMaxGridYZ = 65535;
+inline int check_grid(uint64_t blocks_x, uint64_t threads, uint64_t y, uint64_t z,
+                      const char* who) {
+  if (blocks_x * threads >= (1ull << 32) || blocks_x >= (1ull << 32) || y > kMaxGridYZ ||
+      z > kMaxGridYZ) {
+    set_error(std::string(who) + ": launch too large (grid " + std::to_string(blocks_x) + " x " +
+              std::to_string(y) + " x " + std::to_string(z) + " of " + std::to_string(threads) +
+              " threads): split the call");
+    return kInvalid;
+  }
+  return kOk;
+}
+
 
 }  // namespace fhe
 

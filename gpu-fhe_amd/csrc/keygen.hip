@@ -96,6 +96,7 @@ __global__ __launch_bounds__(kThreads) void k_axpy_const(u64* __restrict__ row,
 int sample(const fhe_ctx* c, u64* out, u64 pstride, u32 polys, u32 limb0, u32 nlimbs, int kind,
            u64 seed, u32 tag, hipStream_t s) {
   if ((u64)polys * nlimbs == 0) return kOk;
+  if (int rc = check_grid(c->n / kThreads, kThreads, nlimbs, polys, "sample")) return rc;
   k_sample<<<dim3((u32)(c->n / kThreads), nlimbs, polys), kThreads, 0, s>>>(
       out, pstride, limb0, c->log_n, kind, (u32)seed, (u32)(seed >> 32), tag, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
@@ -105,6 +106,7 @@ int sample(const fhe_ctx* c, u64* out, u64 pstride, u32 polys, u32 limb0, u32 nl
 int mac_s(const fhe_ctx* c, u64* out, u64 pout, const u64* x, u64 px, const u64* y, u64 py,
           const u64* sk, u32 polys, u32 limb0, u32 nlimbs, bool negate, hipStream_t s) {
   if ((u64)polys * nlimbs == 0) return kOk;
+  if (int rc = check_grid(c->n / kThreads, kThreads, nlimbs, polys, "mac_s")) return rc;
   k_mac_s<<<dim3((u32)(c->n / kThreads), nlimbs, polys), kThreads, 0, s>>>(
       out, pout, x, px, y, py, sk, limb0, c->log_n, negate ? 1 : 0, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());

@@ -1345,7 +1345,8 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
 
 // One workgroup per item, rounded up to a multiple of 8 so item -> XCD placement holds (surplus
 // workgroups exit at once).
-inline dim3 item_grid(u64 items) { return dim3((u32)((items + 7) / 8 * 8)); }
+inline u64 item_blocks(u64 items) { return (items + 7) / 8 * 8; }
+inline dim3 item_grid(u64 items) { return dim3((u32)item_blocks(items)); }
 
 // The inverse passes' H: the lazy inverse does not depend on the forward headroom (one build for
 // H = 8 and 16); wide contexts (H = 2) take the exact one.
@@ -1381,6 +1382,8 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   // the second pass runs in place on dst
   const PolyMap pd = flat_map(dpstride);
   const u64 ic = pl * G::TILES_C;
+  if (int rc = check_grid(item_blocks(ic), G::THR_C, 1, 1, "ntt")) return rc;
+  if (int rc = check_grid(item_blocks(pl * G::TILES_R), G::THR_R, 1, 1, "ntt")) return rc;
   if (fwd) {
     k_ntt_col<LOGN, true, HD>
         <<<item_grid(ic),
@@ -1427,6 +1430,8 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   // over the 4 polys of every ciphertext pair (group of 4: slots 0, 1 from a, slots 2, 3 from b)
   const PolyMap to_x{4, 2 * limbN, limbN, 4 * limbN, limbN, 2};
   const u64 ic = (u64)batch * 4 * nlimbs * G::TILES_C;
+  if (int rc = check_grid(item_blocks(ic), G::THR_C, 1, 1, "hommult")) return rc;
+  if (int rc = check_grid((u64)batch * nlimbs * H::TILES, H::THR, 1, 1, "hommult")) return rc;
   constexpr bool FL = true;  // a, b are read once: non-temporal
   k_ntt_col<LOGN, true, HD, FL><<<item_grid(ic),
                                   G::THR_C, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic,
@@ -1496,12 +1501,14 @@ k_rescale_col(const u64* __restrict__ last, u64* __restrict__ dst, u32 nq, u32 i
 }
 
 template <int LOGN, int HD>
-void rescale_col_dispatch(const fhe_ctx* c, const u64* last, u64* dst, u32 polys, u32 nq,
-                          const u64* half, hipStream_t s) {
+int rescale_col_dispatch(const fhe_ctx* c, const u64* last, u64* dst, u32 polys, u32 nq,
+                         const u64* half, hipStream_t s) {
   using G = Geo<LOGN>;
   const u64 ic = (u64)polys * nq * G::TILES_C;
+  if (int rc = check_grid(item_blocks(ic), G::THR_C, 1, 1, "rescale_col")) return rc;
   k_rescale_col<LOGN, HD><<<item_grid(ic), G::THR_C, 0, s>>>(last, dst, nq, (u32)ic, half,
                                                             c->d_tw_fwd, c->d_mods);
+  return kOk;
 }
 #endif  // !FHE_NTT_KS_ONLY
 
@@ -1519,20 +1526,23 @@ int wide_unsupported() {
   return kUnsupported;
 }
 template <int LOGN, int HD>
-void col_fwd_pass(const fhe_ctx* c, const u64* src, u64 sp, u64* dst, u64 dp, u32 polys,
-                  u32 limb0, u32 nlimbs, hipStream_t s) {
+int col_fwd_pass(const fhe_ctx* c, const u64* src, u64 sp, u64* dst, u64 dp, u32 polys,
+                 u32 limb0, u32 nlimbs, hipStream_t s) {
   using G = Geo<LOGN>;
   const u64 ic = (u64)polys * nlimbs * G::TILES_C;
+  if (int rc = check_grid(item_blocks(ic), G::THR_C, 1, 1, "ntt_col_fwd")) return rc;
   const PolyMap pm{1, sp, 0, dp, 0, 0};
   // scheduled from 2: the row kernels that follow (k_ks_row_inner, k_moddown_row) assume it
   k_ntt_col<LOGN, true, HD, false, false, kFinalInv, 2><<<item_grid(ic),
                               G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic,
                                                 c->d_tw_fwd, c->d_nfold, c->d_mods);
+  return kOk;
 }
 
 template <int LOGN, int HD>
 int ks_row_inner_dispatch(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
   using H = HmGeo<LOGN>;
+  if (int rc = check_grid((u64)a.rows * a.batch * H::TILES, H::THR, 1, 1, "ks_row_inner")) return rc;
   const dim3 g((u32)((u64)a.rows * a.batch * H::TILES));
   switch (c->dnum) {
 #define D(k)                                                                                    \
@@ -1559,10 +1569,11 @@ int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst,
   switch (c->log_n) {
 #define X(n)                                                                                 \
   case n:                                                                                    \
-    if (c->lz16)                                                                             \
-      col_fwd_pass<n, 16>(c, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);        \
-    else                                                                                     \
-      col_fwd_pass<n, 8>(c, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);         \
+    if (int rc = c->lz16 ? col_fwd_pass<n, 16>(c, src, spstride, dst, dpstride, polys, limb0, \
+                                                nlimbs, s)                                   \
+                         : col_fwd_pass<n, 8>(c, src, spstride, dst, dpstride, polys, limb0,  \
+                                              nlimbs, s))                                    \
+      return rc;                                                                             \
     FHE_HIP_CHECK(hipGetLastError());                                                       \
     return kOk;
     FHE_LOGN_CASES(X)
@@ -1578,6 +1589,7 @@ int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
   ModUpYOff yo;
   for (int k = 0; k < 4; ++k) yo.o[k] = a.yoff[k];
   using G = Geo<LOGN>;
+  if (int rc = check_grid((u64)a.T * a.batch * G::TILES_C, G::THR_C, 1, 1, "modup_col")) return rc;
   const dim3 g((u32)((u64)a.T * a.batch * G::TILES_C));
   switch (a.S) {
 #define D(k)                                                                                     \
@@ -1613,12 +1625,14 @@ int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
 
 namespace {
 template <int LOGN, int HD>
-void moddown_row_dispatch(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s) {
+int moddown_row_dispatch(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s) {
   using G = Geo<LOGN>;
   const u64 items = (u64)a.halves * a.batch * a.nq * G::TILES_R;
+  if (int rc = check_grid(item_blocks(items), G::THR_R, 1, 1, "moddown_row")) return rc;
   k_moddown_row<LOGN, HD><<<dim3((u32)((items + 7) / 8 * 8)), G::THR_R, 0, s>>>(
       a.conv, a.ks0, a.ks1, a.acc, a.acc_ws, a.rows, a.nq, a.limb0, a.batch, (u32)items, a.halves,
       a.pinv ? a.pinv : c->d_pinv, c->d_tw_fwd, c->d_mods, a.ep);
+  return kOk;
 }
 }  // namespace
 
@@ -1628,10 +1642,9 @@ int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s)
   switch (c->log_n) {
 #define X(n)                                                                                   \
   case n:                                                                                      \
-    if (c->lz16)                                                                               \
-      moddown_row_dispatch<n, 16>(c, a, s);                                                    \
-    else                                                                                       \
-      moddown_row_dispatch<n, 8>(c, a, s);                                                     \
+    if (int rc = c->lz16 ? moddown_row_dispatch<n, 16>(c, a, s)                              \
+                         : moddown_row_dispatch<n, 8>(c, a, s))                               \
+      return rc;                                                                               \
     FHE_HIP_CHECK(hipGetLastError());                                                         \
     return kOk;
     FHE_LOGN_CASES(X)
@@ -1720,10 +1733,9 @@ int launch_rescale_col(const fhe_ctx* c, const u64* last, u64* dst, u32 polys, u
   switch (c->log_n) {
 #define X(n)                                                  \
   case n:                                                     \
-    if (c->lz16)                                              \
-      rescale_col_dispatch<n, 16>(c, last, dst, polys, nq, half, s); \
-    else                                                      \
-      rescale_col_dispatch<n, 8>(c, last, dst, polys, nq, half, s);  \
+    if (int rc = c->lz16 ? rescale_col_dispatch<n, 16>(c, last, dst, polys, nq, half, s) \
+                         : rescale_col_dispatch<n, 8>(c, last, dst, polys, nq, half, s))  \
+      return rc;                                              \
     FHE_HIP_CHECK(hipGetLastError());                         \
     return kOk;
     FHE_LOGN_CASES(X)

@@ -70,6 +70,7 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   u64* rws = rl + 2 * batch * ln;        // rescale workspace
   u64* kws = reinterpret_cast<u64*>(reinterpret_cast<char*>(rws) +
                                     rescale_workspace_bytes(c, 2 * batch, L));
+  if (int rc = check_grid(n / kThreads, kThreads, L, batch, "tensor_ntt")) return rc;
   const dim3 g((u32)(n / kThreads), L, batch);
   // d2 (NTT form) as a contiguous [batch][L][N] operand for the key-switch: parked in the
   // relinearised-ct buffer, which is free until the combine

@@ -284,6 +284,8 @@ void launch_bc(const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* 
 
 int baseconv_any(u32 S, const BcArgs& a, u64 n, const ulonglong2* inv, const ulonglong2* hat,
                  u32 hs, const ModParams* mods, bool wide, hipStream_t s) {
+  if (int rc = check_grid((n + kThreads - 1) / kThreads, kThreads, a.batch, 1, "baseconv"))
+    return rc;
   switch (S) {
 #define X(k)                                    \
   case k:                                       \
@@ -389,6 +391,10 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     return kUnsupported;
   }
   if (batch == 0) return kOk;
+  // the coefficient-wise kernels put rows on y and (2 x) the batch on y / z
+  if (int rc = check_grid(c->n / kThreads, kThreads, (u64)nlimbs + c->K, 2 * (u64)batch,
+                          "keyswitch"))
+    return rc;
   KsEpilogue ep = epi ? *epi : KsEpilogue{};
   if (ep.out_bs == 0) ep.out_bs = (u64)nlimbs * c->n;
   const u32 L = c->L, K = c->K, M = L + K, alpha = c->alpha, rows = nlimbs + K;
@@ -414,6 +420,19 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   const bool fused_up = fused && alpha <= 4;
   if (call.scaled && !fused_up) {
     set_error("keyswitch: a prepared (pre-scaled) input needs the fused ModUp (ks_prepared)");
+    return kInvalid;
+  }
+  // ModDown's finish: k_moddown_row after the fused conversion (fused_down; a hoisted rotation's
+  // inner step too, with its own scratch for the INTT output) or after k_baseconv (fused), else
+  // the unfused k_moddown_finish
+  const bool fused_down = K <= 4 && ((fused && (u64)c->dnum * rows >= 2 * (u64)K) ||
+                                     (hoist && hoist->ydn && ks_hoist_fused_down(c)));
+  // k_moddown_finish adds its addend rows un-permuted: a sigma-gathered addend
+  // (KsEpilogue::add_gal, which only k_moddown_row implements) reaching it would give a wrong
+  // ciphertext with no error, so a caller whose path predicate (ks_fused / ks_hoist_fused_down)
+  // drifts from this selection is refused before anything is launched
+  if (ep.add_gal && !fused_down && !fused) {
+    set_error("keyswitch: a sigma-gathered epilogue addend needs a k_moddown_row finish");
     return kInvalid;
   }
   if (!hoist || hoist->modup_only) {  // ModUp (a hoisted rotation's inner step skips it)
@@ -487,9 +506,6 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   prof_mark(s, "ks_inner");
   // ModDown: INTT the P rows of both accumulators, convert P -> own Q-limbs, NTT, finish
   u64* accp = acc + (u64)nlimbs * n;
-  // (a hoisted rotation's inner step too, with its own scratch for the INTT output)
-  const bool fused_down = K <= 4 && ((fused && (u64)c->dnum * rows >= 2 * (u64)K) ||
-                                     (hoist && hoist->ydn && ks_hoist_fused_down(c)));
   // Fused ModDown (fused path, K <= 4): the P -> Q conversion runs inside the column-forward
   // pass of the conversion NTT (k_modup_col, as ModUp), on the P rows the INTT has already scaled
   // into the ext region (free once the inner product has run): conv is never written in
@@ -555,11 +571,17 @@ int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u3
       std::vector<Pair64> inv, hat;
       conv_tables(c->moduli, s0, S, inv, hat);
       FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_tab), (inv.size() + hat.size()) * 16));
-      cc->bc_tables.emplace_back(key, d_tab);
-      FHE_HIP_CHECK(hipMemcpyAsync(d_tab, inv.data(), inv.size() * 16, hipMemcpyHostToDevice, s));
-      FHE_HIP_CHECK(hipMemcpyAsync(d_tab + S, hat.data(), hat.size() * 16, hipMemcpyHostToDevice,
-                                   s));
-      FHE_HIP_CHECK(hipStreamSynchronize(s));  // the host vectors must outlive the copies
+      hipError_t e = hipMemcpyAsync(d_tab, inv.data(), inv.size() * 16, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d_tab + S, hat.data(), hat.size() * 16, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);  // the host vectors outlive the copies
+      if (e != hipSuccess) {
+        // never cache a table whose upload did not complete: a later call would read garbage
+        (void)hipFree(d_tab);
+        set_error(std::string("baseconv: table upload: ") + hipGetErrorString(e));
+        return kDevice;
+      }
+      cc->bc_tables.emplace_back(key, d_tab);  // registered only once it is complete
     }
   }
   const BcArgs a{in, 0, rows_contiguous(S, c->n), s0, out, 0, T, RowMap{T, t0, 0}, 0, 0, 1};

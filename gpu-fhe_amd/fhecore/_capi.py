@@ -55,6 +55,15 @@ SIGNATURES = {
     "fhe_keyswitch_dist": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     "fhe_keyswitch_shard_ranked": (_i32, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32,
                                           _u32, _vp, _vp]),
+    "fhe_comm_gather_ms": (_i32, [_vp, ctypes.POINTER(ctypes.c_float), _u32,
+                                  ctypes.POINTER(_u32)]),
+    "fhe_dist_plan_make": (_i32, [_vp, _u32, _u32, _u32, _u32, _u32, _u32]),
+    "fhe_dist_plan_chunk": (_i32, [_vp, _u32, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
+    "fhe_dist_plan_send_word": (_u64, [_vp, _u32, _u32]),
+    "fhe_dist_plan_read_word": (_u64, [_vp, _u32, _u32]),
+    "fhe_keyswitch_dist_loopback_workspace": (_sz, [_vp, _u32, _u32, _u32]),
+    "fhe_keyswitch_dist_loopback": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp,
+                                           _vp]),
     "fhe_rescale_workspace": (_sz, [_vp, _u32, _u32]),
     "fhe_rescale": (_i32, [_vp, _vp, _vp, _u32, _u32, _i32, _vp, _vp]),
     "fhe_automorphism": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _i32, _vp]),
@@ -115,3 +124,12 @@ def check(rc: int, what: str) -> None:
 def u64_array(values):
     arr = (ctypes.c_uint64 * len(values))(*[int(v) for v in values])
     return arr
+
+
+class DistPlan(ctypes.Structure):
+    """fhe_dist_plan (include/fhecore.h): where fhe_keyswitch_dist puts and reads every row."""
+
+    _fields_ = [(f, _u32) for f in ("L", "log_n", "ranks", "rank", "batch", "limb0", "nlimbs",
+                                    "width", "chunks", "chunk_batch")] + \
+               [("block_words", _u64), ("gather_words", _u64)]
+

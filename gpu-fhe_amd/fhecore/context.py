@@ -92,6 +92,18 @@ def _check_tensor(t, what, shape_tail=None):
         raise ValueError(f"{what}: trailing shape {tuple(t.shape)} != (..., {shape_tail})")
 
 
+def _check_out(out, ref, shape, what):
+    """A caller-supplied output: its raw pointer goes straight to a kernel, so it must be a
+    contiguous int64/uint64 HIP tensor of exactly `shape` on the device of `ref` (a CPU tensor or
+    one on another GPU would be written through an invalid device address)."""
+    _check_tensor(out, what)
+    if out.device != ref.device:
+        raise ValueError(f"{what}: on {out.device}, the inputs are on {ref.device}")
+    if tuple(out.shape) != tuple(shape):
+        raise ValueError(f"{what}: shape {tuple(out.shape)} != {tuple(shape)}")
+    return out
+
+
 # ----------------------------------------------------------------------------- context
 
 # Tensors allocated by this module while a Graph is capturing: the captured kernels keep their
@@ -201,8 +213,8 @@ class Context:
         _check_tensor(t, "ntt", (self.n,))
         if out is None:
             out = _empty_like(t)
-        elif out.shape != t.shape or out.dtype != t.dtype or not out.is_contiguous():
-            raise _capi.FheError("ntt: out must be a contiguous tensor shaped like the input")
+        else:
+            _check_out(out, t, t.shape, "ntt: out")
         nl = t.shape[-2] if t.dim() >= 2 else 1
         polys = t.numel() // (nl * self.n)
         fn = load().fhe_ntt_fwd_to if fwd else load().fhe_ntt_inv_to
@@ -225,7 +237,7 @@ class Context:
         _check_tensor(b, op, (self.n,))
         if a.shape != b.shape:
             raise AssertionError("a.shape != b.shape")  # the reference asserts (arithmetic.py:4)
-        out = _empty_like(a) if out is None else out
+        out = _empty_like(a) if out is None else _check_out(out, a, a.shape, op + ": out")
         nl = a.shape[-2] if a.dim() >= 2 else 1
         polys = a.numel() // (nl * self.n)
         fn = {"add": load().fhe_vec_add, "sub": load().fhe_vec_sub, "mul": load().fhe_vec_mul}[op]
@@ -245,7 +257,7 @@ class Context:
         batch = 1 if squeeze else a.shape[0]
         nl = a.shape[-2]
         shape = (3, nl, self.n) if squeeze else (batch, 3, nl, self.n)
-        out = self.empty(*shape) if out is None else out
+        out = self.empty(*shape) if out is None else _check_out(out, a, shape, "hommult: out")
         lib = load()
         ws = workspace
         if ws is None:
@@ -352,8 +364,8 @@ class Context:
         count = len(elts)
         if out is None:
             out = _empty(count, *ct.shape, dtype=ct.dtype, device=ct.device)
-        elif tuple(out.shape) != (count, *ct.shape) or not out.is_contiguous():
-            raise ValueError("rotate_hoisted: out must be a contiguous [count, ..., 2, L, N] tensor")
+        else:
+            _check_out(out, ct, (count, *ct.shape), "rotate_hoisted: out")
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
             lib.fhe_rotate_hoisted_workspace(self._ptr, batch))
@@ -462,8 +474,8 @@ class Context:
         shape = (*a.shape[:-2], self.L - (1 if rescale else 0), self.n)
         if out is None:
             out = _empty(shape, dtype=a.dtype, device=a.device)
-        elif tuple(out.shape) != shape:
-            raise ValueError(f"mul_relin: out must be {shape}")
+        else:
+            _check_out(out, a, shape, "mul_relin: out")
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
             lib.fhe_mul_relin_workspace(self._ptr, batch))
@@ -560,6 +572,47 @@ class Context:
             check(lib.fhe_keyswitch_dist(self._ptr, comm.handle, _ptr(ks0), _ptr(ks1),
                                          _ptr(d2_own), _ptr(evk_b), _ptr(evk_a), batch, chunks,
                                          _ptr(ws), _stream(d2_own)), "fhe_keyswitch_dist")
+        return ks0, ks1
+
+    def keyswitch_dist_loopback(self, d2_parts, evk_b_parts, evk_a_parts, chunks: int = 0,
+                                workspace=None):
+        """fhe_keyswitch_dist's G-rank plan run on this one device (fhe_keyswitch_dist_loopback):
+        per-rank lists (rank r: d2 [batch, nlimbs_r, N] NTT form of LimbShard(L, G, r)'s limbs,
+        evk slices [dnum, nlimbs_r + K, N]; None for ranks owning no limb).  Returns the per-rank
+        (ks0, ks1) lists -- concatenated over the ranks they equal keyswitch()."""
+        G = len(d2_parts)
+        if not G or len(evk_b_parts) != G or len(evk_a_parts) != G:
+            raise ValueError("keyswitch_dist_loopback: one entry per rank in every list")
+        from .dist import LimbShard
+
+        batch = None
+        ks0, ks1 = [None] * G, [None] * G
+        for r in range(G):
+            sh = LimbShard(self.L, G, r)
+            if sh.nlimbs == 0:
+                continue
+            d2 = d2_parts[r]
+            _check_tensor(d2, f"d2[{r}]", (sh.nlimbs, self.n))
+            for t, nm in ((evk_b_parts[r], "evk_b"), (evk_a_parts[r], "evk_a")):
+                _check_tensor(t, f"{nm}[{r}]", (self.dnum, sh.nlimbs + self.K, self.n))
+                if t.device != d2.device:
+                    raise ValueError("keyswitch_dist_loopback: every tensor on one device")
+            b = d2.numel() // (sh.nlimbs * self.n)
+            if batch is not None and b != batch:
+                raise ValueError("keyswitch_dist_loopback: every rank needs the same batch")
+            batch = b
+            ks0[r], ks1[r] = _empty_like(d2), _empty_like(d2)
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_keyswitch_dist_loopback_workspace(self._ptr, G, batch, chunks))
+        arr = lambda ts: (ctypes.c_void_p * G)(*[t.data_ptr() if t is not None else None  # noqa: E731
+                                                  for t in ts])
+        ref = next(t for t in d2_parts if t is not None)
+        with torch.cuda.device(self.device):
+            check(lib.fhe_keyswitch_dist_loopback(self._ptr, G, arr(ks0), arr(ks1), arr(d2_parts),
+                                                  arr(evk_b_parts), arr(evk_a_parts), batch,
+                                                  chunks, _ptr(ws), _stream(ref)),
+                  "fhe_keyswitch_dist_loopback")
         return ks0, ks1
 
 

@@ -76,6 +76,17 @@ class LimbShard:
         return cls(L, 1, 0)
 
 
+def dist_plan(L: int, log_n: int, ranks: int, rank: int, batch: int, chunks: int = 0):
+    """libfhecore's placement plan of fhe_keyswitch_dist for one rank (fhe_dist_plan_make; host
+    only, no GPU needed): limb window, chunking and the gather region's geometry."""
+    from ._capi import DistPlan, check, load
+
+    p = DistPlan()
+    check(load().fhe_dist_plan_make(ctypes.byref(p), L, log_n, ranks, rank, batch, chunks),
+          "fhe_dist_plan_make")
+    return p
+
+
 def gather_ranked(x_own, shard: LimbShard, group=None):
     """[..., nlimbs, N] per rank -> [world, batch, width, N] on every rank (batch = the flattened
     leading dims; blocks shorter than `width` padded): one all_gather_into_tensor, no reorder."""
@@ -159,6 +170,16 @@ class RcclComm:
     @property
     def handle(self):
         return self._c
+
+    def gather_ms(self):
+        """Per-chunk all-gather durations (ms, on the communicator's stream) of the last
+        keyswitch_dist call (fhe_comm_gather_ms; waits for those gathers)."""
+        from ._capi import check, load
+
+        ms = (ctypes.c_float * 16)()
+        cnt = ctypes.c_uint32()
+        check(load().fhe_comm_gather_ms(self._c, ms, 16, ctypes.byref(cnt)), "fhe_comm_gather_ms")
+        return [float(v) for v in ms[:cnt.value]]
 
     def shard(self, L: int) -> LimbShard:
         return LimbShard(L, self.world, self.rank)

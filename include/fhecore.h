@@ -175,6 +175,44 @@ int fhe_keyswitch_shard_ranked(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1,
                                const uint64_t* evk_b, const uint64_t* evk_a, uint32_t limb0,
                                uint32_t nlimbs, uint32_t batch, void* workspace,
                                fhe_stream_t stream);
+/* Per-chunk all-gather durations (ms, HIP events on the communicator's stream) of the last
+ * fhe_keyswitch_dist call on `comm`: waits for that call's gathers; *count = its chunk count. */
+int fhe_comm_gather_ms(fhe_comm_t comm, float* ms, uint32_t cap, uint32_t* count);
+
+/* The placement plan fhe_keyswitch_dist follows (host only: no device access, callable without a
+ * GPU).  Rank `rank` of `ranks` owns Q-limbs [limb0, limb0 + nlimbs); the batch is cut into
+ * `chunks` chunks of `chunk_batch` ciphertexts (the last one possibly shorter, none empty); per
+ * chunk every rank contributes one block of chunk_batch x width x N words (width = ceil(L / ranks),
+ * padded on ranks owning fewer limbs), and the all-gather leaves the blocks rank-major in a region
+ * of gather_words words: [chunks][ranks][chunk_batch][width][N].
+ * fhe_dist_plan_chunk: the chunk's first ciphertext and length.
+ * fhe_dist_plan_send_word: word offset in the gather region where this rank writes row (ciphertext
+ * b, own limb j); fhe_dist_plan_read_word: where the key-switch reads row (b, Q-limb l) -- the
+ * addressing its kernels use.  UINT64_MAX for an out-of-range argument. */
+typedef struct fhe_dist_plan {
+  uint32_t L, log_n, ranks, rank, batch;
+  uint32_t limb0, nlimbs, width;
+  uint32_t chunks, chunk_batch;
+  uint64_t block_words, gather_words;
+} fhe_dist_plan;
+int fhe_dist_plan_make(fhe_dist_plan* plan, uint32_t L, uint32_t log_n, uint32_t ranks,
+                       uint32_t rank, uint32_t batch, uint32_t chunks);
+int fhe_dist_plan_chunk(const fhe_dist_plan* plan, uint32_t k, uint32_t* b0, uint32_t* bn);
+uint64_t fhe_dist_plan_send_word(const fhe_dist_plan* plan, uint32_t b, uint32_t j);
+uint64_t fhe_dist_plan_read_word(const fhe_dist_plan* plan, uint32_t b, uint32_t l);
+
+/* fhe_keyswitch_dist for `ranks` ranks run one after another on this context's device (a
+ * loopback communicator: the ranks' INTTs write one shared gather region, which is exactly what
+ * the all-gather would leave on every rank).  Executes the G-rank plan, offsets and chunking of
+ * fhe_keyswitch_dist on one GPU; per-rank arguments are host arrays of `ranks` device pointers
+ * (ranks owning no limb may pass NULL), laid out as fhe_keyswitch_dist's. */
+size_t fhe_keyswitch_dist_loopback_workspace(const fhe_ctx* ctx, uint32_t ranks, uint32_t batch,
+                                             uint32_t chunks);
+int fhe_keyswitch_dist_loopback(const fhe_ctx* ctx, uint32_t ranks, uint64_t* const* ks0,
+                                uint64_t* const* ks1, const uint64_t* const* d2_own,
+                                const uint64_t* const* evk_b, const uint64_t* const* evk_a,
+                                uint32_t batch, uint32_t chunks, void* workspace,
+                                fhe_stream_t stream);
 
 /* ---- rescale and rotation (not in the reference) ---------------------
  * Standard RNS-CKKS operations on this library's layout, restated by oracle/pyoracle.py

@@ -55,6 +55,8 @@ def lib():
         L.port_keyswitch.argtypes = [_u64p, _u64p, _u64p, _u64p, _u64p, u64, u32, _u64p, u32,
                                      _u64p, u32, u32]
         L.port_keyswitch.restype = None
+        L.port_vec_op.argtypes = [i32, _u64p, _u64p, _u64p, u64, u64, _u64p]
+        L.port_vec_op.restype = None
         _lib = L
     return _lib
 
@@ -141,6 +143,19 @@ def port_ntt(x, moduli, forward=True) -> np.ndarray:
     fn = lib().port_ntt_fwd if forward else lib().port_ntt_inv
     fn(_p(x), x.size // (L * n), n.bit_length() - 1, _p(m), L)
     return x
+
+
+def port_vec_op(op: str, a, b, mods_per_row, out=None) -> np.ndarray:
+    """The tuned port's vec_add / vec_sub / vec_mul on canonical [rows, cols] residues, row r
+    modulo mods_per_row[r] (bench.py --workload vec cpu_baseline)."""
+    a2 = np.ascontiguousarray(_u64(a).reshape(-1, a.shape[-1]))
+    b2 = np.ascontiguousarray(_u64(b).reshape(a2.shape))
+    m = np.ascontiguousarray(_u64(mods_per_row).reshape(-1))
+    assert m.size == a2.shape[0]
+    o = np.empty_like(a2) if out is None else out.reshape(a2.shape)
+    lib().port_vec_op({"add": 0, "sub": 1, "mul": 2}[op], _p(o), _p(a2), _p(b2), a2.shape[0],
+                      a2.shape[1], _p(m))
+    return o.reshape(a.shape)
 
 
 def port_hommult_into(d, a, b, moduli) -> None:

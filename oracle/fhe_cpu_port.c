@@ -395,3 +395,31 @@ void port_keyswitch(u64* ks0, u64* ks1, const u64* d2, const u64* evk_b, const u
   }
   free(mods); free(red); free(uinv); free(uinvs); free(uhat); free(dhat); free(y); free(acc); free(yp);
 }
+
+/* ---------------------------------------------------------------- vec_add / vec_sub / vec_mul
+ * The reference's coefficient-wise operators (/root/reference/arithmetic.py:3-13, exact
+ * semantics) on canonical residues a, b, out [rows][cols], row r modulo mods[r], the way a tuned
+ * CPU library would run them: OpenMP over rows, no `%` -- add / sub by one conditional
+ * correction, mul by a 64x64 -> 128 product reduced by red128 (two Shoup products).  Timed as
+ * bench.py --workload vec's cpu_baseline; checked against oracle_vec_op by tests/test_oracle.py. */
+void port_vec_op(int op, u64* out, const u64* a, const u64* b, uint64_t rows, uint64_t cols,
+                 const u64* mods) {
+#pragma omp parallel for schedule(static)
+  for (int64_t r = 0; r < (int64_t)rows; ++r) {
+    const u64 q = mods[r];
+    const u64* x = a + (u64)r * cols;
+    const u64* y = b + (u64)r * cols;
+    u64* o = out + (u64)r * cols;
+    if (op == 0) {
+      for (u64 c = 0; c < cols; ++c) {
+        const u64 s = x[c] + y[c];
+        o[c] = s >= q ? s - q : s;
+      }
+    } else if (op == 1) {
+      for (u64 c = 0; c < cols; ++c) o[c] = x[c] >= y[c] ? x[c] - y[c] : x[c] + q - y[c];
+    } else {
+      const red_t rd = red_make(q);
+      for (u64 c = 0; c < cols; ++c) o[c] = red128((u128)x[c] * y[c], &rd);
+    }
+  }
+}

@@ -64,6 +64,15 @@ def test_errors_are_reported_not_raised():
     assert lib.fhe_ntt_inv_to(None, None, None, 1, 0, 1, None) == -1
     assert lib.fhe_vec_add(None, None, None, None, 1, 0, 1, None) == -1
     assert lib.fhe_hommult_workspace(None, 1, 1) == 0
+    assert lib.fhe_keyswitch_dist(None, None, None, None, None, None, None, 1, 0, None,
+                                  None) == -1
+    assert lib.fhe_keyswitch_dist_loopback(None, 2, None, None, None, None, None, 1, 0, None,
+                                           None) == -1
+    assert lib.fhe_keyswitch_dist_loopback_workspace(None, 2, 1, 0) == 0
+    assert lib.fhe_comm_gather_ms(None, None, 0, None) == -1
+    # a null key pointer inside the hoisted rotation's key arrays is refused before
+    # anything reaches the device (a context is needed first, so only the null context here)
+    assert lib.fhe_rotate_hoisted(None, None, None, None, None, None, 1, 1, None, None) == -1
 
 
 def test_ctx_create_validates_moduli_before_touching_a_device():

@@ -70,6 +70,44 @@ def test_ranked_gather_layout_shards(fc, log_n, L, K, dnum, G, batch):
                             1, ranks=G)
 
 
+@pytest.mark.parametrize("log_n,L,K,dnum,G,batch,chunks", [
+    (16, 16, 4, 4, 8, 4, 4),   # configs[3] at 8 ranks, the bench's chunking (1 ciphertext each)
+    (16, 16, 4, 4, 2, 5, 4),   # 2 ranks, uneven chunks (2, 2, 1)
+    (14, 16, 4, 4, 4, 6, 0),   # default chunking
+    (12, 16, 4, 4, 6, 3, 2),   # uneven shards 3,3,3,3,3,1
+    (12, 10, 2, 3, 8, 2, 2),   # ranks without limbs
+    (12, 10, 2, 2, 3, 7, 16),  # more chunks asked than ciphertexts
+])
+def test_keyswitch_dist_loopback_g_ranks(fc, log_n, L, K, dnum, G, batch, chunks):
+    """fhe_keyswitch_dist's G-rank plan executed on this GPU (fhe_keyswitch_dist_loopback: every
+    virtual rank's INTT writes its block of one gather region -- what the in-place all-gather
+    leaves on each rank -- then every rank's chunked key-switch reads it through CAll::ranked):
+    the G > 1 offsets, chunking and rank blocks of the native multi-GPU path, bit-exact against
+    the single-device key-switch."""
+    from fhecore.dist import LimbShard
+
+    ctx = fc.Context(log_n, L=L, K=K, dnum=dnum)
+    d2 = rand(ctx.moduli, log_n, (batch,), seed=G + batch)
+    eb = rand(ctx.all_moduli, log_n, (dnum,), seed=5)
+    ea = rand(ctx.all_moduli, log_n, (dnum,), seed=6)
+    full0, full1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(eb), fc.to_device(ea))
+    parts = [[], [], []]
+    for r in range(G):
+        sh = LimbShard(L, G, r)
+        if sh.nlimbs == 0:
+            for p in parts:
+                p.append(None)
+            continue
+        rows = sh.evk_rows(K)
+        parts[0].append(fc.to_device(np.ascontiguousarray(d2[:, sh.lo:sh.hi])))
+        parts[1].append(fc.to_device(np.ascontiguousarray(eb[:, rows])))
+        parts[2].append(fc.to_device(np.ascontiguousarray(ea[:, rows])))
+    k0, k1 = ctx.keyswitch_dist_loopback(*parts, chunks=chunks)
+    got0 = np.concatenate([fc.to_host(t) for t in k0 if t is not None], axis=1)
+    got1 = np.concatenate([fc.to_host(t) for t in k1 if t is not None], axis=1)
+    assert (got0 == fc.to_host(full0)).all() and (got1 == fc.to_host(full1)).all()
+
+
 @pytest.mark.parametrize("batch,chunks", [(1, 0), (4, 0), (5, 4), (3, 8), (6, 2)])
 def test_keyswitch_dist_one_rank_rccl(fc, batch, chunks):
     """fhe_keyswitch_dist through a real RCCL communicator (world 1): INTT into the gather buffer,
@@ -90,4 +128,10 @@ def test_keyswitch_dist_one_rank_rccl(fc, batch, chunks):
     assert (fc.to_host(k0) == fc.to_host(r0)).all() and (fc.to_host(k1) == fc.to_host(r1)).all()
     o0, o1 = coracle.keyswitch(d2[0], eb, ea, ctx.moduli, ctx.special, dnum)
     assert (fc.to_host(k0)[0] == o0).all() and (fc.to_host(k1)[0] == o1).all()
+    # one timed all-gather per chunk of the plan
+    from fhecore.dist import dist_plan
+
+    ms = comm.gather_ms()
+    assert len(ms) == dist_plan(L, log_n, 1, 0, batch, chunks).chunks
+    assert all(v >= 0 for v in ms)
     comm.close()

@@ -128,3 +128,45 @@ def test_hommult_rank_shapes_of_the_scaling_bench(fc, world):
     for sl in (slice(0, 2), slice(B - 2, B)):
         want = coracle.hommult(fc.to_host(a[sl]), fc.to_host(b[sl]), mods)
         assert (fc.to_host(d[sl]) == want).all()
+
+
+def test_configs4_full_batch_round_trip(fc):
+    """BASELINE configs[4] at its full size on one GPU: 1024 polynomials x 32 limbs x N = 2^17
+    (2^32 residues, 32 GiB) -- the whole batch through the forward NTT (first and last
+    polynomial compared with the C oracle) and back through the inverse (every word compared
+    with a device copy of the input)."""
+    import torch
+
+    log_n, L, P = 17, 32, 1024
+    n = 1 << log_n
+    ctx = fc.Context(log_n, L=L)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1024)
+    x = torch.empty(P, L, n, dtype=torch.int64, device="cuda")
+    for l, q in enumerate(ctx.moduli):  # uniform residues, one limb at a time (bounded temporaries)
+        x[:, l, :] = torch.randint(0, q, (P, n), generator=gen, dtype=torch.int64, device="cuda")
+    keep = x.clone()
+    ctx.ntt_(x)
+    for p in (0, P - 1):
+        assert (fc.to_host(x[p]) == coracle.ntt_fwd(fc.to_host(keep[p]), ctx.moduli)).all()
+    ctx.intt_(x)
+    torch.cuda.synchronize()
+    assert torch.equal(x, keep)
+    del x, keep
+    torch.cuda.empty_cache()
+
+
+def test_oversize_launch_is_refused(fc):
+    """Launch sizes are checked before any kernel is launched (csrc/internal.hpp check_grid): a
+    grid dimension the dispatch cannot hold returns FHE_EINVAL instead of being truncated.  Here
+    70000 polynomials at N = 2^10 put 70000 workgroups on the automorphism's z dimension (at most
+    65535); the buffers are real, so nothing could fault even if the check were missing."""
+    import torch
+
+    ctx = fc.Context(10, L=1)
+    x = torch.zeros(70000, 1, 1 << 10, dtype=torch.int64, device="cuda")
+    with pytest.raises(fc.FheError, match="launch too large"):
+        ctx.automorphism(x, 5)
+    # one poly fewer than the limit still runs
+    y = ctx.automorphism(x[:65535], 5)
+    assert tuple(y.shape) == (65535, 1, 1 << 10)

@@ -161,7 +161,11 @@ def _real_ct(ctx, log_n, rng):
     return ct.astype(np.uint64), s, s_n, m
 
 
-@pytest.mark.parametrize("log_n,L,K,dnum", [(10, 3, 2, 3), (11, 4, 2, 2)])
+@pytest.mark.parametrize("log_n,L,K,dnum", [
+    (10, 3, 2, 3), (11, 4, 2, 2),
+    # the branches with an unfused ModDown -- K > 4 (the separate sigma(c0) pass,
+    # k_moddown_finish) and dnum > 4 (k_ks_inner's u128 sums with the gather)
+    (10, 6, 5, 2), (10, 6, 2, 6)])
 def test_rotate_hoisted_matches_oracle_and_decrypts(fc, log_n, L, K, dnum):
     """fhe_rotate_hoisted (one ModUp, the automorphism gathered inside the inner product) bit-exact
     vs pyoracle.rotate_hoisted for several Galois elements at once; every output decrypts to the
@@ -208,3 +212,29 @@ def test_rotate_hoisted_batch_matches_single_and_errors(fc):
     assert (fc.to_host(ctx.rotate_hoisted(d(ct), ks[1:], dk[1:]))[0] == batched[1]).all()
     with pytest.raises(fc.FheError):
         ctx.rotate_hoisted(d(ct), [4], dk[:1])  # even Galois element
+    # a caller-supplied out must be a HIP int64/uint64 tensor on the ct's device
+    import torch
+
+    shape = (2, 3, 2, L, 1 << log_n)
+    with pytest.raises(TypeError):
+        ctx.rotate_hoisted(d(ct), ks, dk, out=torch.empty(shape, dtype=torch.int64))  # on CPU
+    with pytest.raises(TypeError):
+        ctx.rotate_hoisted(d(ct), ks, dk, out=torch.empty(shape, dtype=torch.float64,
+                                                          device="cuda"))
+    with pytest.raises(ValueError):
+        ctx.rotate_hoisted(d(ct), ks, dk, out=torch.empty((1,) + shape[1:], dtype=torch.int64,
+                                                          device="cuda"))
+    # ... and a null key pointer inside the per-rotation arrays is refused at the C ABI
+    import ctypes
+
+    from fhecore import _capi
+
+    lib = _capi.load()
+    ctd = d(ct)
+    out = torch.empty(shape, dtype=torch.int64, device="cuda")
+    g_arr = (ctypes.c_uint32 * 2)(*ks)
+    b_arr = (ctypes.c_void_p * 2)(dk[0][0].data_ptr(), None)
+    a_arr = (ctypes.c_void_p * 2)(dk[0][1].data_ptr(), dk[1][1].data_ptr())
+    rc = lib.fhe_rotate_hoisted(ctx.handle, out.data_ptr(), ctd.data_ptr(), g_arr, b_arr, a_arr,
+                                2, 3, None, None)
+    assert rc == -1 and b"null key pointer" in lib.fhe_last_error()

@@ -190,6 +190,36 @@ def test_hommult_reference_composed_golden(fc, fx):
     assert (got[1] == d["d"][::-1]).all()
 
 
+def test_hommult_config3_full_size_reference_sampled(fc):
+    """BASELINE configs[2] at its full size -- N = 2^16, the 8-limb chain, the bench's batch of 64
+    through the bench's kernels -- against the reference's own arithmetic: 48 output coefficients
+    of d0, d1, d2 of one ciphertext pair (at batch index 37), each computed by
+    tests/golden/make_golden.py with only /root/reference/arithmetic.py:3-13 (one vec_mul of a
+    against b's signed reversal, a vec_add halving tree).  The pair is regenerated from the
+    fixture's seed and checked by sha256 before the comparison; the other 63 pairs are random.
+    The whole batch is also checked against the C oracle on two more pairs."""
+    import hashlib
+    import sys
+
+    sys.path.insert(0, GOLDEN)
+    from make_golden import sampled_inputs  # data generation only (seeded numpy)
+
+    d = np.load(os.path.join(GOLDEN, "hommult_sampled_N65536_L8.npz"))
+    log_n, qs = int(d["log_n"]), [int(q) for q in d["moduli"]]
+    n = 1 << log_n
+    pa, pb = sampled_inputs(qs, n, int(d["seed"]))
+    assert hashlib.sha256(pa.tobytes() + pb.tobytes()).hexdigest() == str(d["inputs_sha256"])
+    ctx = fc.Context(log_n, moduli=qs)
+    B, at = 64, 37
+    a = rand(qs, log_n, (B, 2), seed=98)
+    b = rand(qs, log_n, (B, 2), seed=99)
+    a[at], b[at] = pa, pb
+    got = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
+    assert (got[at][:, :, d["index"]].transpose(2, 0, 1) == d["d"]).all()
+    for i in (0, B - 1):
+        assert (got[i] == coracle.hommult(a[i], b[i], qs)).all()
+
+
 @pytest.mark.parametrize("op", ["add", "sub", "mul"])
 def test_vec_config3_chain_golden(fc, op):
     """vec_* on the configs[2] chain: the first 4096 coefficients of each N = 2^16 limb are the

@@ -54,6 +54,27 @@ def test_oracle_hommult_matches_reference_composed_product(fx):
     assert (coracle.hommult(a, b, mods)[0] == d["d"]).all()
 
 
+def test_oracle_hommult_config3_full_size_matches_reference_samples():
+    """BASELINE configs[2] at full size (N = 2^16, 8 limbs): the oracle's HomMult reproduces the 48
+    output coefficients of d0, d1, d2 that make_golden.py computed with only the reference's own
+    vec_mul / vec_sub / vec_add (hommult_sampled_N65536_L8.npz); the regenerated inputs match the
+    fixture's sha256."""
+    import hashlib
+    import sys
+
+    sys.path.insert(0, GOLDEN)
+    from make_golden import sampled_inputs
+
+    d = _load("hommult_sampled_N65536_L8.npz")
+    mods = [int(q) for q in d["moduli"]]
+    assert mods == pyoracle.gen_moduli(16, 8)
+    a, b = sampled_inputs(mods, 1 << int(d["log_n"]), int(d["seed"]))
+    assert hashlib.sha256(a.tobytes() + b.tobytes()).hexdigest() == str(d["inputs_sha256"])
+    got = coracle.hommult(a[None], b[None], mods)[0]
+    assert len(d["index"]) == 48
+    assert (got[:, :, d["index"]].transpose(2, 0, 1) == d["d"]).all()
+
+
 def test_reference_uint64_divergence_is_recorded():
     """The reference's uint64 path is wrong for sub (a<b) and mul (wraps): the build targets exact
     semantics; the fixture keeps the reference's uint64 outputs to document the divergence."""
@@ -305,6 +326,14 @@ def test_cpu_port_matches_oracle(log_n, bits):
     a = np.stack([rng.integers(0, q, (2, 2, n), dtype=np.uint64) for q in mods], axis=2)
     b = np.stack([rng.integers(0, q, (2, 2, n), dtype=np.uint64) for q in mods], axis=2)
     assert (coracle.port_hommult(a, b, mods) == coracle.hommult(a, b, mods)).all()
+    # the tuned vec ops (bench.py --workload vec cpu_baseline) against the exact checker, with
+    # q - 1 / 0 edge values
+    va = np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in mods])
+    vb = np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in mods])
+    va[:, :4] = np.asarray(mods, dtype=np.uint64)[:, None] - 1
+    vb[:, 2:6] = 0
+    for op in ("add", "sub", "mul"):
+        assert (coracle.port_vec_op(op, va, vb, mods) == coracle.vec_op(op, va, vb, mods)).all()
 
 
 @pytest.mark.parametrize("log_n,L,K,dnum", [(10, 4, 2, 2), (11, 5, 2, 3), (10, 6, 3, 6), (12, 16, 4, 4)])
