@@ -609,20 +609,28 @@ class KeyswitchLeg:
         self.evk_a = uniform_limbs(gen, [allm[r] for r in rows], (self.DNUM,), n)
         self.B = args.ks_batch
         self.d2 = uniform_limbs(gen, ctx.moduli[self.shard.lo:self.shard.hi], (self.B,), n)
-        self.comm = fdist.RcclComm()
         self.chunks = args.ks_chunks or (1 if world == 1 else 4)
-        self.ws = ctx.workspace(load().fhe_keyswitch_dist_workspace(ctx.handle, self.comm.handle,
-                                                                    self.B, self.chunks))
+        # the native path needs one GPU per rank (RCCL refuses two ranks on one device); the
+        # gloo rehearsal of several ranks on one GPU takes the torch.distributed form instead
+        # (fhecore.dist.sharded_keyswitch: INTT, one all_gather through the host, local step)
+        self.native = world == 1 or torch.distributed.get_backend() == "nccl"
+        if self.native:
+            self.comm = fdist.RcclComm()
+            self.ws = ctx.workspace(load().fhe_keyswitch_dist_workspace(
+                ctx.handle, self.comm.handle, self.B, self.chunks))
 
     def step(self):
-        self.ctx.keyswitch_dist(self.comm, self.d2, self.evk_b, self.evk_a, chunks=self.chunks,
-                                workspace=self.ws)
+        if self.native:
+            self.ctx.keyswitch_dist(self.comm, self.d2, self.evk_b, self.evk_a,
+                                    chunks=self.chunks, workspace=self.ws)
+        else:
+            fdist.sharded_keyswitch(self.ctx, self.d2, self.evk_b, self.evk_a, self.shard)
 
     def run(self, targs):
         L, K, dnum, B, world = self.L, self.K, self.DNUM, self.B, self.world
         n = 1 << self.log_n
         dt, kavg = timed(self.step, targs, world, 64 * targs.steps + 64)
-        gather = self.comm.gather_ms()  # the last call's chunks
+        gather = self.comm.gather_ms() if self.native else []  # the last call's chunks
         ks_per_s = B * targs.steps / dt
         ms_per_ks = dt / (B * targs.steps) * 1e3
         # d2 in + evk (dnum * 2 * (L + K) limbs) + 2 L limbs out per key-switch; the
@@ -632,15 +640,18 @@ class KeyswitchLeg:
                "ms_per_step": round(dt / targs.steps * 1e3, 4),
                "config": {"workload": "hybrid key-switch, BASELINE configs[3] (fhe_keyswitch_dist)",
                           "log_n": self.log_n, "L": L, "K": K, "dnum": dnum, "batch": B,
-                          "chunks": self.chunks, "scaling": "strong",
-                          "parallelism": f"rns-limb-shard x{world}, RCCL all-gather"},
+                          "chunks": self.chunks if self.native else 1, "scaling": "strong",
+                          "parallelism": f"rns-limb-shard x{world}, " + (
+                              "RCCL all-gather in libfhecore (fhe_keyswitch_dist)" if self.native
+                              else "torch.distributed all_gather (gloo, host-staged; "
+                                   "fhecore.dist.sharded_keyswitch)")},
                "warmup": targs.warmup, "steps": targs.steps,
                "gather_ms_per_chunk": [round(v, 4) for v in gather],
                "keyswitch_alg_hbm_gbps_per_gpu": round(ks_per_s * alg / 1e9 / world, 1),
                "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
                "roofline": roofline("keyswitch (whole, per GPU)", alg // world, ms_per_ks,
                                     {"log_n": self.log_n, "L": L, "world": world})}
-        plan = fdist.dist_plan(L, self.log_n, world, self.rank, B, self.chunks)
+        plan = fdist.dist_plan(L, self.log_n, world, self.rank, B, self.chunks if self.native else 1)
         res["gather_bytes_per_chunk"] = plan.block_words * 8 * world  # what each rank ends up with
         # integer-ALU roofline of one key-switch on this rank, butterflies only: INTT of the own
         # d2 limbs; ModUp: every digit's extended rows = dnum (nl + K) - nl forward NTTs; ModDown:

@@ -102,6 +102,12 @@ def gather_ranked(x_own, shard: LimbShard, group=None):
     x = x.contiguous()
     if shard.world == 1:
         return x.reshape(1, lead, shard.width, n)
+    if x.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo gathers host tensors only: the multi-rank rehearsal on one GPU (several ranks
+        # sharing a device, where RCCL refuses duplicate GPUs) stages through the host
+        buf = torch.empty((shard.world * lead, shard.width, n), dtype=x.dtype)
+        dist.all_gather_into_tensor(buf, x.cpu(), group=group)
+        return buf.to(x.device).view(shard.world, lead, shard.width, n)
     buf = torch.empty((shard.world * lead, shard.width, n), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(buf, x, group=group)
     return buf.view(shard.world, lead, shard.width, n)
