@@ -287,7 +287,6 @@ def run_hommult(args, world, rank):
     # NTT throughput rides along (BASELINE metric "NTTs/sec"): forward + inverse NTTs of 64 polys
     # on this rank's limbs, sustained (warmed up, then timed like the main leg), every NTT counted
     x = uniform_limbs(gen, mods, (64,), n)
-    ks = None if args.no_keyswitch_leg or args.bits != 60 else KeyswitchLeg(args, world, rank)
 
     def ntt_pair():
         ctx.ntt_(x, limb0=shard.lo)
@@ -336,8 +335,10 @@ def run_hommult(args, world, rank):
         out["roofline"]["frac"] else "hbm"
     if args.bits != 60:
         out["config"]["modulus_bits"] = args.bits
-    if ks is not None:
-        out["keyswitch_leg"] = ks.run(argparse.Namespace(warmup=20, steps=50))
+    if not (args.no_keyswitch_leg or args.bits != 60):
+        out["keyswitch_leg"] = guarded_leg(
+            lambda: KeyswitchLeg(args, world, rank).run(argparse.Namespace(warmup=20, steps=50)),
+            out, rank, "keyswitch_leg")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_hommult(ctx.moduli, args.log_n, args.cpu_seconds)
@@ -877,6 +878,51 @@ def cpu_baseline_rotate(moduli, special, log_n, dnum, budget_s):
                       f"key-switch, OpenMP {cpu_threads()} threads, in {dt:.1f} s"}
 
 
+_EMIT = {}  # json_fd, args, world: what emit_line needs (set by main)
+
+
+def emit_line(out, cpu):
+    """Rank 0's one JSON line on the saved stdout."""
+    args, world = _EMIT["args"], _EMIT["world"]
+    out = dict(out)
+    line = {"metric": out.pop("metric"), "value": out.pop("value"), "unit": out.pop("unit"),
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": out.pop("ms_per_step"), "higher_is_better": True,
+            "scaling": out.pop("scaling", "weak"),
+            "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (uniform residues per RNS limb, seeded)",
+            "config": out.pop("config")}
+    line.update(out)
+    line["cpu_baseline"] = cpu
+    sys.stdout.flush()
+    os.write(_EMIT["json_fd"], (json.dumps(line) + "\n").encode())
+
+
+def guarded_leg(fn, out, rank, name, timeout_s=180.0):
+    """Runs a ride-along leg after the headline is measured, so that nothing it does can cost the
+    headline line: an exception becomes {"error": ...} in the line, and a leg still running after
+    `timeout_s` (e.g. a collective that never completes on some node) makes rank 0 print the line
+    without it and every rank exit."""
+    import threading
+
+    def fire():
+        if rank == 0:
+            o = dict(out)
+            o[name] = {"error": f"did not finish within {timeout_s:.0f} s; line emitted without it"}
+            emit_line(o, None)
+        os._exit(0)
+
+    timer = threading.Timer(timeout_s, fire)
+    timer.daemon = True
+    timer.start()
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 -- reported in the line, the headline stands
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        timer.cancel()
+
+
 def main():
     # stdout carries exactly one JSON line: anything else the libraries print there (RCCL prints
     # its version banner to stdout when a communicator comes up) is sent to stderr
@@ -889,21 +935,12 @@ def main():
     if args.batch is None:
         args.batch = 64 if args.workload == "hommult" else 16
     world, rank = dist_setup(args)
+    _EMIT.update(json_fd=json_fd, args=args, world=world)
     run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch, "vec": run_vec,
            "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch, "rotate": run_rotate}[args.workload]
     out, cpu = run(args, world, rank)
     if rank == 0:
-        line = {"metric": out.pop("metric"), "value": out.pop("value"), "unit": out.pop("unit"),
-                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                "ms_per_step": out.pop("ms_per_step"), "higher_is_better": True,
-                "scaling": out.pop("scaling", "weak"),
-                "vs_baseline": None, "dtype": "u64",
-                "data": "synthetic (uniform residues per RNS limb, seeded)",
-                "config": out.pop("config")}
-        line.update(out)
-        line["cpu_baseline"] = cpu
-        sys.stdout.flush()
-        os.write(json_fd, (json.dumps(line) + "\n").encode())
+        emit_line(out, cpu)
     if world > 1:
         torch.distributed.destroy_process_group()
 

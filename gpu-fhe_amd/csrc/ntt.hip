@@ -723,8 +723,8 @@ struct Geo {
 // follows must assume the same R0: fwd_range is not monotonic in it (an earlier reduction can leave
 // a smaller bound), so the key-switch / rescale row kernels, which assume 2 (k_modup_col's
 // outputs), get column passes scheduled from 2 as well (col_fwd_pass, k_rescale_col).
-// One column tile (poly p, limb l, tile) of a column pass: the body of k_ntt_col and of the fused
-// single-launch NTT (k_ntt_fused).  lds: G::LDS_C words.
+// One column tile (poly p, limb l, tile) of a column pass (the body of k_ntt_col; lds: G::LDS_C
+// words).
 template <int LOGN, bool FWD, int H, bool NTL, bool NTS, int FI, int R0>
 __device__ __forceinline__ void col_tile(u64* lds, const u64* __restrict__ src,
                                          const u64* __restrict__ src2, u64* __restrict__ dst,
@@ -779,9 +779,9 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 
                                            pl % nlimbs, tile, tw_all, nfold, mods);
 }
 
-// One row tile (poly p, limb l, tile) of a row pass: the body of k_ntt_row and of k_ntt_fused.
+// One row tile (poly p, limb l, tile) of a row pass (the body of k_ntt_row; lds: G::LDS_R words).
 // The forward stores its last round in linear order through the LDS (XOUT); the inverse loads its
-// first round that way.  lds: G::LDS_R words.
+// first round that way.
 template <int LOGN, bool FWD, int H, bool NTL, bool NTS>
 __device__ __forceinline__ void row_tile(u64* lds, const u64* __restrict__ src,
                                          u64* __restrict__ dst, u32 limb0, const PolyMap& pm,
@@ -1475,149 +1475,6 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   FHE_HIP_CHECK(hipGetLastError());
   return kOk;
 }
-// ---- single-launch NTT, L2-resident intermediate (EXPERIMENT) -------------------
-// Both passes of an NTT in one persistent launch: workgroups pull tickets from a per-XCD queue
-// (the queue of the XCD they run on, read from the hardware register), and every poly-limb's two
-// passes are issued through the same queue, first pass before second, with `lag` poly-limbs
-// between them, so the intermediate (one poly-limb: N words) is produced and consumed inside one
-// XCD's L2 instead of making a round trip through HBM.  Hand-off: the first-pass workgroup drains
-// its stores (vmcnt(0): in the XCD's L2), then adds 1 to the poly-limb's counter (agent-scope
-// atomic); a second-pass workgroup polls that counter until every first-pass tile of its
-// poly-limb has arrived and reads the intermediate with L1-bypassing (nt) loads.  Same-XCD
-// producer and consumer is what makes plain stores visible without an L2 write-back; it holds by
-// construction (a ticket is only taken from the queue of the XCD the workgroup runs on).
-// Deadlock-free: a second-pass ticket waits only for first-pass tickets of its queue that were
-// taken earlier, by workgroups that never wait.  Needs every XCD to run workgroups of the grid
-// (fhe_x_xcc_census checks the dispatch at run time).
-__device__ __forceinline__ u32 xcc_id() {
-  u32 x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return x;
-}
-
-__global__ void k_xcc_census(u32* hist, u32* map) {
-  if (threadIdx.x == 0) {
-    u32 raw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(raw));
-    atomicAdd(hist + (xcc_id() & 15), 1u);
-    if (map) map[blockIdx.x] = raw;
-  }
-}
-
-// Ticket t of a queue holding m poly-limbs (index i), first pass TA tiles, second TB tiles, lag g:
-// [A(0) .. A(g-1)] then per j: [A(j + g), B(j)], then the last g B's.  Returns false past the end.
-__device__ __forceinline__ bool fused_ticket(u32 t, u32 m, u32 g, u32 TA, u32 TB, u32& phase,
-                                             u32& i, u32& tile) {
-  g = g < m ? g : m;
-  if (t < g * TA) {
-    phase = 0, i = t / TA, tile = t % TA;
-    return true;
-  }
-  u32 u = t - g * TA;
-  const u32 blk = TA + TB, mid = m - g;
-  if (u < mid * blk) {
-    const u32 j = u / blk, r = u % blk;
-    if (r < TA) phase = 0, i = j + g, tile = r;
-    else phase = 1, i = j, tile = r - TA;
-    return true;
-  }
-  u -= mid * blk;
-  if (u >= g * TB) return false;
-  phase = 1, i = mid + u / TB, tile = u % TB;
-  return true;
-}
-
-template <int LOGN, bool FWD, int H>
-__global__ FHE_KATTR void k_ntt_fused(const u64* __restrict__ src, u64 sp, u64* __restrict__ dst,
-                                      u64 dp, u32 nlimbs, u32 limb0, u32 P, u32 nq, u32 lag,
-                                      u32* __restrict__ ctr, const ulonglong2* __restrict__ tw_all,
-                                      const ulonglong2* __restrict__ nfold,
-                                      const ModParams* __restrict__ mods) {
-  using G = Geo<LOGN>;
-  static_assert(G::THR_C == kThreads && G::THR_R == kThreads, "one block size for both passes");
-  constexpr u32 LW = G::LDS_C > G::LDS_R ? G::LDS_C : G::LDS_R;
-  __shared__ u64 lds[LW];
-  __shared__ u32 s_tk;
-  constexpr u32 TA = FWD ? G::TILES_C : G::TILES_R, TB = FWD ? G::TILES_R : G::TILES_C;
-  const u32 x = xcc_id() % nq;
-  const u32 m = x < P ? (P - 1 - x) / nq + 1 : 0;  // poly-limbs pl = x, x + nq, ... < P
-  u32* head = ctr + x;
-  u32* done = ctr + nq;
-  const PolyMap pm{1, sp, 0, dp, 0, 0}, pd{1, dp, 0, dp, 0, 0};
-  // (src2 is never selected: alt = 0; passing a null literal there crashes the ROCm 7.2 LLVM
-  // optimizer, so the real source pointer goes in its place)
-  // the next ticket, uniform over the workgroup (lane 0 takes it, the LDS broadcasts it)
-  auto next = [&]() -> u32 {
-    if (threadIdx.x == 0)
-      s_tk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const u32 v = __builtin_amdgcn_readfirstlane(s_tk);
-    __syncthreads();
-    return v;
-  };
-  u32 phase = 0, i = 0, tile = 0;
-  u32 t = next();
-  while (fused_ticket(t, m, lag, TA, TB, phase, i, tile)) {
-    const u32 pl = i * nq + x, p = pl / nlimbs, l = pl % nlimbs;
-    if (phase == 0) {
-      if constexpr (FWD)
-        col_tile<LOGN, true, H, false, false, kFinalInv, 1>(lds, src, src, dst, limb0, pm, p,
-                                                             l, tile, tw_all, nfold, mods);
-      else
-        row_tile<LOGN, false, H, false, false>(lds, src, dst, limb0, pm, p, l, tile, tw_all, mods);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are in the L2
-      __syncthreads();
-      if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(done + pl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (threadIdx.x == 0) {
-        // bounded: a broken hand-off flags ctr[nq + P] and ends the kernel with wrong output
-        // instead of a hung GPU
-        u32 spins = 0;
-        while (__hip_atomic_load(done + pl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < TA &&
-               spins < (1u << 16)) {
-          __builtin_amdgcn_s_sleep(2);
-          ++spins;
-        }
-        if (spins >= (1u << 16))
-          __hip_atomic_store(done + P, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      if constexpr (FWD)
-        row_tile<LOGN, true, H, true, false>(lds, dst, dst, limb0, pd, p, l, tile, tw_all, mods);
-      else
-        col_tile<LOGN, false, H, true, false, kFinalInv, 1>(lds, dst, dst, dst, limb0, pd, p,
-                                                            l, tile, tw_all, nfold, mods);
-    }
-    t = next();
-  }
-}
-
-template <int LOGN, int HD>
-int ntt_fused_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 sp, u64* dst, u64 dp,
-                       u32 polys, u32 limb0, u32 nlimbs, u32 lag, u32 wgs, u32 nq, u32* ctr,
-                       hipStream_t s) {
-  using G = Geo<LOGN>;
-  if constexpr (G::THR_C != kThreads || G::THR_R != kThreads) {
-    set_error("ntt_fused: N = 2^14 .. 2^17 only");
-    return kUnsupported;
-  } else {
-    const u32 P = polys * nlimbs;
-    FHE_HIP_CHECK(hipMemsetAsync(ctr, 0, (size_t)(nq + P + 1) * sizeof(u32), s));
-    if (fwd)
-      k_ntt_fused<LOGN, true, HD><<<wgs, kThreads, 0, s>>>(src, sp, dst, dp, nlimbs, limb0, P, nq,
-                                                          lag, ctr, c->d_tw_fwd, c->d_nfold,
-                                                          c->d_mods);
-    else
-      k_ntt_fused<LOGN, false, inv_h(HD)><<<wgs, kThreads, 0, s>>>(src, sp, dst, dp, nlimbs, limb0,
-                                                                  P, nq, lag, ctr, c->d_tw_inv,
-                                                                  c->d_nfold, c->d_mods);
-    prof_mark(s, fwd ? "ntt_fused_fwd" : "ntt_fused_inv");
-    FHE_HIP_CHECK(hipGetLastError());
-    return kOk;
-  }
-}
-
 // Rescale (NTT form): the spread of the last limb over the other limbs folded into the
 // column-forward pass.  last [polys][N] holds INTT(x_last); the tile of limb l (l < nq, the last
 // limb is nq) loads last's columns and spreads them in registers,
@@ -1889,51 +1746,6 @@ int launch_hommult(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 bat
   if ((u64)batch * nlimbs == 0) return kOk;
   return hommult_chunk(c, d, a, b, batch, limb0, nlimbs, static_cast<u64*>(ws), s);
 }
-
-}  // namespace fhe
-
-// Experimental entry points (not in include/fhecore.h; tools/time_ntt_fused.py binds them):
-// the XCD census of a grid and the single-launch NTT above.
-extern "C" int fhe_x_xcc_census(int device, uint32_t blocks, uint32_t* hist16, uint32_t* map) {
-  using namespace fhe;
-  FHE_HIP_CHECK(hipSetDevice(device));
-  u32* d = nullptr;
-  FHE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), (16 + (size_t)blocks) * sizeof(u32)));
-  FHE_HIP_CHECK(hipMemset(d, 0, (16 + (size_t)blocks) * sizeof(u32)));
-  k_xcc_census<<<blocks, 64>>>(d, d + 16);
-  FHE_HIP_CHECK(hipGetLastError());
-  FHE_HIP_CHECK(hipMemcpy(hist16, d, 16 * sizeof(u32), hipMemcpyDeviceToHost));
-  if (map) FHE_HIP_CHECK(hipMemcpy(map, d + 16, blocks * sizeof(u32), hipMemcpyDeviceToHost));
-  FHE_HIP_CHECK(hipFree(d));
-  return kOk;
-}
-
-extern "C" int fhe_x_ntt_fused(const fhe_ctx* c, int forward, uint64_t* data, uint32_t polys,
-                               uint32_t limb0, uint32_t nlimbs, uint32_t lag, uint32_t wgs,
-                               uint32_t nq, uint32_t* ctr, void* stream) {
-  using namespace fhe;
-  if (!c || !ctr || nq == 0 || wgs == 0 || (u64)limb0 + nlimbs > c->L + c->K || c->wide) {
-    set_error("fhe_x_ntt_fused: bad arguments");
-    return kInvalid;
-  }
-  if ((u64)polys * nlimbs == 0) return kOk;
-  const hipStream_t s = static_cast<hipStream_t>(stream);
-  const u64 ps = (u64)nlimbs * c->n;
-  switch (c->log_n) {
-#define X(n)                                                                                 \
-  case n:                                                                                    \
-    return c->lz16 ? ntt_fused_dispatch<n, 16>(c, forward, data, ps, data, ps, polys, limb0,  \
-                                               nlimbs, lag, wgs, nq, ctr, s)                 \
-                   : ntt_fused_dispatch<n, 8>(c, forward, data, ps, data, ps, polys, limb0,   \
-                                              nlimbs, lag, wgs, nq, ctr, s);
-    X(14) X(15) X(16) X(17)
-#undef X
-  }
-  set_error("fhe_x_ntt_fused: N = 2^14 .. 2^17 only");
-  return kUnsupported;
-}
-
-namespace fhe {
 
 int launch_rescale_col(const fhe_ctx* c, const u64* last, u64* dst, u32 polys, u32 nq,
                        const u64* half, hipStream_t s) {
