@@ -284,9 +284,11 @@ def run_hommult(args, world, rank):
     d = ctx.empty(gbatch, 3, shard.nlimbs, n)
     ws = ctx.workspace(load().fhe_hommult_workspace(ctx.handle, gbatch, shard.nlimbs))
     step = lambda: fdist.sharded_hommult(ctx, a, b, shard, out=d, workspace=ws)  # noqa: E731
-    # NTT throughput rides along (BASELINE metric "NTTs/sec"): forward + inverse NTTs of 64 polys
-    # on this rank's limbs, sustained (warmed up, then timed like the main leg), every NTT counted
-    x = uniform_limbs(gen, mods, (64,), n)
+    # NTT throughput rides along (BASELINE metric "NTTs/sec"): forward + inverse NTTs of 512
+    # poly-limbs per GPU (64 polys x 8 limbs at N = 1; the same count of this rank's limbs above, so
+    # per-GPU work stays fixed like the HomMult leg's), sustained, every NTT counted
+    npolys = 64 * L // max(shard.nlimbs, 1)
+    x = uniform_limbs(gen, mods, (npolys,), n)
 
     def ntt_pair():
         ctx.ntt_(x, limb0=shard.lo)
@@ -294,7 +296,7 @@ def run_hommult(args, world, rank):
 
     nargs = argparse.Namespace(warmup=100, steps=200)
     ntt_dt, ntt_k = timed(ntt_pair, nargs, world, 8 * nargs.steps + 8)
-    ntt_per_s = 2 * 64 * shard.nlimbs * world * nargs.steps / ntt_dt
+    ntt_per_s = 2 * npolys * shard.nlimbs * world * nargs.steps / ntt_dt
 
     dt, kavg = timed(step, args, world, 8 * args.steps + 8)
     hm_per_s = gbatch * args.steps / dt  # each rank covers its limbs of all gbatch pairs
@@ -310,7 +312,7 @@ def run_hommult(args, world, rank):
                    "log_n": args.log_n, "limbs": L, "batch_per_gpu": args.batch,
                    "global_batch": gbatch, "parallelism": f"rns-limb-shard x{world}"},
         "ntt_per_sec": round(ntt_per_s, 1),
-        "ntt_config": {"log_n": args.log_n, "direction": "forward+inverse", "polys": 64,
+        "ntt_config": {"log_n": args.log_n, "direction": "forward+inverse", "polys_per_gpu": npolys,
                        "limbs_per_gpu": shard.nlimbs, "warmup": nargs.warmup,
                        "steps": nargs.steps, "order": "run before the HomMult leg"},
         "ntt_kernel_ms": {k: round(v, 4) for k, v in ntt_k.items()},
