@@ -113,18 +113,25 @@ def uniform_limbs(gen, moduli, lead, n):
 
 
 def timed(fn, args, world, max_marks):
-    """Warmup, then exactly `steps` calls between barrier+sync brackets, with launch marks."""
+    """Warmup, then exactly `steps` calls between barrier+sync brackets with nothing else on the
+    stream; then the same `steps` calls again with a HIP-event mark after each launch group, whose
+    averages are the per-kernel durations (kernel_ms, roofline.achieved).  The marks stay out of
+    the timed window: each record costs ~4 us of idle GPU between kernels (rocprofv3 trace,
+    DESIGN.md §6)."""
     for _ in range(args.warmup):
         fn()
     barrier(world)
-    lib = load()
-    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    check(lib.fhe_prof_begin(max_marks, stream), "fhe_prof_begin")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         fn()
     barrier(world)
     dt = time.perf_counter() - t0
+    lib = load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    check(lib.fhe_prof_begin(max_marks, stream), "fhe_prof_begin")
+    for _ in range(args.steps):
+        fn()
+    barrier(world)
     ms = (ctypes.c_float * max_marks)()
     cnt = ctypes.c_uint32()
     names = ctypes.create_string_buffer(32 * max_marks + 64)

@@ -142,6 +142,9 @@ struct ModUpColArgs {
   u32 hs;
 };
 int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s);
+// several digits (n <= 4) of one ModUp: one launch for each run of digits with the same S and
+// shared fields
+int launch_modup_cols(const fhe_ctx* c, const ModUpColArgs* a, u32 n, hipStream_t s);
 // ModDown finish fused into the conversion NTT's row-forward pass (ntt.hip, k_moddown_row): conv
 // [2][batch][nq][N] column-passed -> ks{0,1} [batch][nq][N] = (acc - NTT(conv)) P^-1 mod q.
 // Optional epilogue of a key-switch's ModDown finish: the outputs of ciphertext b land at

@@ -1013,9 +1013,17 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   });
 }
 
-// The digit's source rows (kernel argument): row k of ciphertext b at y + b ybs + o[k].
-struct ModUpYOff {
+// Up to 4 digits of one ModUp in one launch (kernel argument).  Digit k owns the blocks from
+// blk0 on; its source row j of ciphertext b is at y + b ybs + o[j], its T target rows go to ext.
+struct ModUpDigit {
   u64 o[4];
+  u64* ext;
+  const ulonglong2* hat;
+  u32 T, skip_at, skip_len, blk0;
+};
+struct ModUpDigits {
+  ModUpDigit d[4];
+  u32 n;
 };
 
 // ModUp column pass (key-switch): the column-forward pass of every extended row of one digit,
@@ -1028,18 +1036,14 @@ struct ModUpYOff {
 // is k_baseconv + k_ntt_col).  Items (target row, ciphertext, column tile) are dealt XCD-major,
 // target fastest: an XCD converts every target of a (ciphertext, tile) while the S source tiles are
 // hot in its L2.  Target tr -> row r = tr < skip_at ? tr : tr + skip_len (the digit's own rows are
-// skipped) -> limb r < n0 ? base0 + r : base1 + (r - n0).
+// skipped) -> limb r < n0 ? base0 + r : base1 + (r - n0).  Every digit of a ModUp runs in this
+// one launch (md.n digits with the same S, block ranges in digit order: no launch tail per digit).
 template <int LOGN, int H, int S>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
-    4, 8))) void k_modup_col(const u64* __restrict__ y,
-                                                        u64 ybs, ModUpYOff yoff,
-                                                        u64* __restrict__ ext, u64 rn, u32 T,
-                                                        u32 skip_at, u32 skip_len, u32 n0,
-                                                        u32 base0, u32 base1, u32 batch,
-                                                        const ulonglong2* __restrict__ hat,
-                                                        u32 hs,
-                                                        const ulonglong2* __restrict__ tw_all,
-                                                        const ModParams* __restrict__ mods) {
+    4, 8))) void k_modup_col(const u64* __restrict__ y, u64 ybs, const ModUpDigits md, u64 rn,
+                             u32 n0, u32 base0, u32 base1, u32 batch, u32 hs,
+                             const ulonglong2* __restrict__ tw_all,
+                             const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
   using Rd = Rounds<G::N1>;
   using Lay0 = Layout<G::N1, Rd::kb(0), Rd::lo_fwd(0)>;
@@ -1047,15 +1051,24 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   __shared__ u64 lds[G::LDS_C];
   const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
   const LViewC<G::SUBS_C> lv{lds + sub};
+  u32 di = 0;
+#pragma unroll
+  for (u32 k = 1; k < 4; ++k)
+    if (k < md.n && blockIdx.x >= md.d[k].blk0) di = k;
+  const ModUpDigit& dg = md.d[di];
+  const u32 T = dg.T, skip_at = dg.skip_at, skip_len = dg.skip_len;
+  u64* __restrict__ ext = dg.ext;
+  const ulonglong2* __restrict__ hat = dg.hat;
+  const u32 blk = blockIdx.x - dg.blk0;
   const u32 nbt = batch * G::TILES_C;
   u32 tr, bt;
-  if (nbt % 8 == 0) {
-    const u32 xcd = blockIdx.x % 8, k8 = blockIdx.x / 8;
+  if (nbt % 8 == 0) {  // every digit's block range then starts at a multiple of 8
+    const u32 xcd = blk % 8, k8 = blk / 8;
     tr = k8 % T;
     bt = xcd + 8 * (k8 / T);
   } else {
-    tr = blockIdx.x % T;
-    bt = blockIdx.x / T;
+    tr = blk % T;
+    bt = blk / T;
   }
   const u32 b = bt / G::TILES_C, tile = bt % G::TILES_C;
   const u32 r = tr < skip_at ? tr : tr + skip_len;
@@ -1077,7 +1090,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
       u64 ys[S];
 #pragma unroll
-      for (int k = 0; k < S; ++k) ys[k] = yb[yoff.o[k] + i];
+      for (int k = 0; k < S; ++k) ys[k] = yb[dg.o[k] + i];
       u64 tlo, thi;
       dot_wide61<S>(ys, hk, tlo, thi);
       x[j] = mont_redc(tlo, thi, m.q, qi);  // (0, 2q): the pass takes inputs below 2q
@@ -1093,7 +1106,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
       Sum30 acc;
 #pragma unroll
-      for (int k = 0; k < S; ++k) acc.add(yb[yoff.o[k] + i], h2[k]);
+      for (int k = 0; k < S; ++k) acc.add(yb[dg.o[k] + i], h2[k]);
       x[j] = acc.mont_lazy(m.q, m.qinv);  // [0, 2q): the pass takes inputs below 2q
     }
   }
@@ -1608,19 +1621,33 @@ int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst,
 }
 
 namespace {
+// a[0..n) share everything but the per-digit fields (yoff, ext, T, skip_*, hat): one launch
 template <int LOGN, int HD>
-int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
-  ModUpYOff yo;
-  for (int k = 0; k < 4; ++k) yo.o[k] = a.yoff[k];
+int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs* a, u32 n, hipStream_t s) {
   using G = Geo<LOGN>;
-  if (int rc = check_grid((u64)a.T * a.batch * G::TILES_C, G::THR_C, 1, 1, "modup_col")) return rc;
-  const dim3 g((u32)((u64)a.T * a.batch * G::TILES_C));
-  switch (a.S) {
-#define D(k)                                                                                     \
-  case k:                                                                                        \
-    k_modup_col<LOGN, HD, k><<<g, G::THR_C, 0, s>>>(a.y, a.ybs, yo, a.ext, a.rn, a.T, a.skip_at,  \
-                                                    a.skip_len, a.n0, a.base0, a.base1, a.batch, \
-                                                    a.hat, a.hs, c->d_tw_fwd, c->d_mods);        \
+  ModUpDigits md{};
+  md.n = n;
+  u64 blocks = 0;
+  for (u32 k = 0; k < n; ++k) {
+    ModUpDigit& d = md.d[k];
+    for (int j = 0; j < 4; ++j) d.o[j] = a[k].yoff[j];
+    d.ext = a[k].ext;
+    d.hat = a[k].hat;
+    d.T = a[k].T;
+    d.skip_at = a[k].skip_at;
+    d.skip_len = a[k].skip_len;
+    d.blk0 = (u32)blocks;
+    blocks += (u64)a[k].T * a[k].batch * G::TILES_C;
+    if (int rc = check_grid(blocks, G::THR_C, 1, 1, "modup_col")) return rc;
+  }
+  const ModUpColArgs& a0 = a[0];
+  const dim3 g((u32)blocks);
+  switch (a0.S) {
+#define D(k)                                                                                   \
+  case k:                                                                                      \
+    k_modup_col<LOGN, HD, k><<<g, G::THR_C, 0, s>>>(a0.y, a0.ybs, md, a0.rn, a0.n0, a0.base0, \
+                                                    a0.base1, a0.batch, a0.hs, c->d_tw_fwd,    \
+                                                    c->d_mods);                                \
     break;
     D(1) D(2) D(3) D(4)
 #undef D
@@ -1633,18 +1660,44 @@ int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
 }
 }  // namespace
 
-int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
-  if ((u64)a.T * a.batch == 0) return kOk;
-  if (c->wide) return wide_unsupported();
+namespace {
+int launch_modup_group(const fhe_ctx* c, const ModUpColArgs* a, u32 n, hipStream_t s) {
   switch (c->log_n) {
-#define X(n) \
-  case n:    \
-    return c->lz16 ? modup_col_dispatch<n, 16>(c, a, s) : modup_col_dispatch<n, 8>(c, a, s);
+#define X(n_) \
+  case n_:    \
+    return c->lz16 ? modup_col_dispatch<n_, 16>(c, a, n, s) : modup_col_dispatch<n_, 8>(c, a, n, s);
     FHE_LOGN_CASES(X)
 #undef X
   }
   set_error("unsupported log_n");
   return kUnsupported;
+}
+}  // namespace
+
+int launch_modup_cols(const fhe_ctx* c, const ModUpColArgs* a, u32 n, hipStream_t s) {
+  if (c->wide) return wide_unsupported();
+  // digits with no targets launch nothing; consecutive digits whose shared fields agree (always,
+  // within one key-switch, except a last digit with fewer limbs) go in one launch
+  ModUpColArgs live[4];
+  u32 m = 0;
+  for (u32 k = 0; k < n; ++k) {
+    const ModUpColArgs& x = a[k];
+    if ((u64)x.T * x.batch == 0) continue;
+    const bool joins = m > 0 && m < 4 && x.y == live[0].y && x.ybs == live[0].ybs &&
+                       x.rn == live[0].rn && x.S == live[0].S && x.n0 == live[0].n0 &&
+                       x.base0 == live[0].base0 && x.base1 == live[0].base1 &&
+                       x.batch == live[0].batch && x.hs == live[0].hs;
+    if (m > 0 && !joins) {
+      if (int rc = launch_modup_group(c, live, m, s)) return rc;
+      m = 0;
+    }
+    live[m++] = x;
+  }
+  return m ? launch_modup_group(c, live, m, s) : kOk;
+}
+
+int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s) {
+  return launch_modup_cols(c, &a, 1, s);
 }
 
 namespace {

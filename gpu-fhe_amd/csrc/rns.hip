@@ -441,7 +441,10 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     return fused ? launch_ntt_col_fwd(c, p, rn, p, rn, batch, l0, nl, s)
                  : launch_ntt(c, true, p, p, batch, rn, l0, nl, s);
   };
-  // ModUp + NTT, per digit, for every row outside the digit itself
+  // ModUp + NTT, per digit, for every row outside the digit itself.  Prepared inputs (no
+  // per-digit scaling pass into the shared yws) put every digit's conversion pass in one launch.
+  ModUpColArgs pend[4];
+  u32 npend = 0;
   for (u32 j = 0; j < c->dnum; ++j) {
     const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
     u64* e = ext + (u64)j * B * rn;
@@ -470,6 +473,10 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
       const ModUpColArgs ma{ysrc, ybs, {yoff[0], yoff[1], yoff[2], yoff[3]}, e, rn, S,
                             rows - skip_len, skip_at, skip_len, nlimbs, limb0, L, batch,
                             c->d_modup_hat + (size_t)j * alpha * M, M};
+      if (call.scaled && npend < 4) {
+        pend[npend++] = ma;
+        continue;
+      }
       if ((rc = launch_modup_col(c, ma, s))) return rc;
       continue;
     }
@@ -484,6 +491,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     if (b1 > b0 && (rc = ntt_fwd(e + (u64)(b0 - limb0) * n, b0, b1 - b0))) return rc;
     if ((rc = ntt_fwd(e + (u64)nlimbs * n, L, K))) return rc;
   }
+  if (npend && (rc = launch_modup_cols(c, pend, npend, s))) return rc;
   prof_mark(s, "ks_modup");
   if (hoist) return kOk;  // modup_only: the NTT-form digits stay in the workspace's ext region
   }
