@@ -32,6 +32,12 @@ int check_window(const fhe_ctx* c, uint32_t limb0, uint32_t nlimbs, uint32_t lim
 // Internal workspace (grows on demand).  Refused while `s` is capturing a graph: growing it would
 // free memory a captured graph still points at, and a graph sharing it with eager calls on other
 // streams would race them, so captured calls must bring their own workspace.
+// Calls on different streams are ordered: a call whose stream differs from the last user's first
+// waits (host side, hipDeviceSynchronize) until the device has finished what was queued before it,
+// which includes the last call's launches since calls sharing the internal workspace are issued
+// one after another by the host (concurrent host threads must pass their own workspaces,
+// fhecore.h).  The last user's stream is not touched again: the caller may have destroyed it.
+// Growing the buffer waits the same way before the old one is freed.
 int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws, hipStream_t s) {
   if (*ws) return kOk;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -41,13 +47,18 @@ int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws, hipStream_t s) {
     return kInvalid;
   }
   auto* c = const_cast<fhe_ctx*>(cc);
-  if (c->workspace_bytes < bytes) {
+  std::lock_guard<std::mutex> lock(c->ws_mutex);
+  const bool grow = c->workspace_bytes < bytes;
+  if (c->ws_used && (c->ws_stream != s || grow)) FHE_HIP_CHECK(hipDeviceSynchronize());
+  if (grow) {
     if (c->workspace) FHE_HIP_CHECK(hipFree(c->workspace));
     c->workspace = nullptr;
     c->workspace_bytes = 0;
     FHE_HIP_CHECK(hipMalloc(&c->workspace, bytes));
     c->workspace_bytes = bytes;
   }
+  c->ws_stream = s;
+  c->ws_used = true;
   *ws = c->workspace;
   return kOk;
 }

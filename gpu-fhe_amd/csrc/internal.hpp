@@ -91,6 +91,11 @@ struct fhe_ctx {
 
   void* workspace = nullptr;
   size_t workspace_bytes = 0;
+  // the stream that last took the internal workspace (a call on another stream waits for the
+  // device first: capi.cpp ensure_ws)
+  hipStream_t ws_stream = nullptr;
+  bool ws_used = false;
+  std::mutex ws_mutex;
   // fhe_baseconv's conversion tables per source range (s0, S): device [S] inv + [S][L + K] hat,
   // built on first use (rns.hip launch_baseconv) and freed with the context
   std::mutex bc_mutex;

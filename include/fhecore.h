@@ -20,8 +20,11 @@
  *    layout [poly][limb][N] (limb-major, each limb's N coefficients contiguous).
  *  - `stream` is a hipStream_t (NULL = the legacy default stream).  Launches are
  *    asynchronous and capture-safe (no allocation or synchronisation inside) unless noted.
- *  - A context is immutable after creation: calls on different streams may share it, except
- *    that passing workspace == NULL uses the context's internal workspace (not thread-safe).
+ *  - A context is immutable after creation: calls on different streams may share it.  Passing
+ *    workspace == NULL uses the context's internal workspace: a call on a different stream
+ *    than the previous such call first waits for the device (hipDeviceSynchronize), so calls
+ *    issued one after another never overlap on it; host threads calling concurrently must each
+ *    pass their own workspace.
  *  - limb0 / nlimbs select a contiguous window of the context's Q-limbs (RNS-limb sharding).
  */
 #ifndef FHECORE_H

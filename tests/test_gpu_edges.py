@@ -170,3 +170,34 @@ def test_oversize_launch_is_refused(fc):
     # one poly fewer than the limit still runs
     y = ctx.automorphism(x[:65535], 5)
     assert tuple(y.shape) == (65535, 1, 1 << 10)
+
+
+def test_internal_workspace_shared_across_streams(fc):
+    """workspace == NULL on alternating streams (include/fhecore.h conventions): every call uses
+    the context's one internal buffer, so a call on another stream must not start before the
+    previous call has finished with it.  Two different HomMult batches on two streams, issued
+    back to back several times, each still equal to the same product computed alone."""
+    import torch
+    from fhecore._capi import check, load
+
+    lib = load()
+    log_n, L, B = 14, 4, 8
+    ctx = fc.Context(log_n, L=L)
+    n = 1 << log_n
+    mods = list(ctx.moduli)
+    ins = [tuple(fc.to_device(rand(mods, log_n, (B, 2), seed=s + k)) for k in (0, 1))
+           for s in (11, 23)]
+    want = [ctx.hommult(a, b).cpu() for a, b in ins]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.empty(B, 3, L, n, dtype=torch.int64, device="cuda") for _ in ins]
+    torch.cuda.synchronize()
+    for _ in range(4):
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()
+        for (a, b), o, s in zip(ins, outs, streams):  # back to back, no host sync in between
+            check(lib.fhe_hommult(ctx.handle, o.data_ptr(), a.data_ptr(), b.data_ptr(), B, 0, L,
+                                  None, s.cuda_stream), "fhe_hommult")
+        torch.cuda.synchronize()
+        for o, w in zip(outs, want):
+            assert torch.equal(o.cpu(), w)
