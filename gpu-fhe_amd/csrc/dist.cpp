@@ -282,7 +282,7 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
   void* kws = gather + p.gather_words;
   // 1 + 2: every chunk's INTT into its send block, then its gather on the comm stream.  With one
   // chunk nothing could overlap the gather, so it runs on the caller's stream: a cross-stream
-  // event hand-off costs ~40 us of idle GPU per call (measured, DESIGN.md §7).
+  // event hand-off costs ~40 us of idle GPU per call (measured, DESIGN.md §8).
   const bool own_stream = p.chunks > 1;
   const hipStream_t gs = own_stream ? comm->stream : s;
   for (u32 k = 0; k < p.chunks; ++k) {
