@@ -821,8 +821,10 @@ __device__ __forceinline__ void row_tile(u64* lds, const u64* __restrict__ src,
                 tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, mods[limb].q, {0, 0}, {0, 0});
 }
 
-// Row pass, one workgroup per item (l, p, tile): the limb follows the XCD and the poly varies
-// fastest, so the workgroups of one XCD reuse a row's twiddles while they are hot.
+// Row pass, one workgroup per item (l, p, tile): the limb follows the XCD (its row twiddles stay
+// in that XCD's L2) and the tile varies fastest, so an XCD streams each poly-limb's rows front to
+// back.  (Poly fastest, which re-read a row's twiddles sooner: row passes 8 % slower,
+// profiles/r03_row_order_ab.txt.)
 template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false>
 __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src, u64* __restrict__ dst, u32 nlimbs,
                                     u32 limb0, PolyMap pm, u32 items,
@@ -830,13 +832,12 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src, u64* __restrict
                                     const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
   __shared__ u64 lds[G::LDS_R];
-  const u32 polys = items / (nlimbs * G::TILES_R);
   const u32 it = blockIdx.x;
   if (it >= items) return;
   u32 l, rest;
   xcd_limb_split(it, nlimbs, items / nlimbs, l, rest);
-  row_tile<LOGN, FWD, H, NTL, NTS>(lds, src, dst, limb0, pm, rest % polys, l, rest / polys, tw_all,
-                                   mods);
+  row_tile<LOGN, FWD, H, NTL, NTS>(lds, src, dst, limb0, pm, rest / G::TILES_R, l,
+                                   rest % G::TILES_R, tw_all, mods);
 }
 
 // Fused HomMult row kernel: rows of the 4 column-transformed inputs (layout [batch][4][nlimbs][N]
@@ -886,9 +887,11 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   __shared__ u64 lds[H::ROWS * H::ROWW];
   u32 l, rest;
   xcd_limb_split(blockIdx.x, nlimbs, gridDim.x / nlimbs, l, rest);
-  // ciphertext fastest: consecutive workgroups of one XCD reuse a row's twiddles while hot
-  const u32 batch = gridDim.x / (nlimbs * H::TILES);
-  const u32 b = rest % batch, tile = rest / batch;
+  // tile fastest: an XCD's workgroups stream each poly-limb's rows front to back (DRAM page
+  // locality; the limb's row twiddles stay in that XCD's L2 either way).  Measured against
+  // ciphertext fastest: hm_row_tensor 0.684 -> 0.668 ms, standalone row passes -8 %
+  // (profiles/r03_row_order_ab.txt)
+  const u32 b = rest / H::TILES, tile = rest % H::TILES;
   const u32 limb = limb0 + l;
   const ModParams m = mods[limb];
   const u64 q = m.q;
@@ -1190,10 +1193,10 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   const LView<1, true> lv{lds + sub * G::RS};
   const u32 it = blockIdx.x;
   if (it >= items) return;
-  const u32 polys = halves * batch;
+  (void)halves;  // items = nq * halves * batch * TILES_R
   u32 l, rest;
   xcd_limb_split(it, nq, items / nq, l, rest);
-  const u32 p = rest % polys, tile = rest / polys;
+  const u32 p = rest / G::TILES_R, tile = rest % G::TILES_R;  // tile fastest, as k_ntt_row
   const u32 h = p / batch, b = p % batch;
   const u32 row0 = tile * G::SUBS_R;
   const u32 limb = __builtin_amdgcn_readfirstlane(limb0 + l);
@@ -1239,16 +1242,19 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
   using Rd = Rounds<G::N2>;
   constexpr u64 N = 1ull << LOGN;
   __shared__ u64 lds[H::ROWS * H::ROWW];
-  // XCD-major placement, ciphertext fastest: the workgroups of one XCD run all `batch` ciphertexts
-  // of a (row, tile) back to back, so that tile's key words and twiddles are read from HBM once
-  // and served from that XCD's L2 for the rest (gridDim.x = rows * TILES * batch, TILES % 8 == 0)
+  // Placement: tile t goes to XCD t mod 8, and the 8 XCDs sweep one (row, ciphertext) together,
+  // the TILES / 8 tiles of each XCD back to back, ciphertexts of a row next: a row's ext words
+  // stream contiguously, and an XCD's share of the row's key words and twiddles (its tiles) stays
+  // in its L2 for all `batch` ciphertexts.  (Ciphertext fastest per (row, tile), round 2: this
+  // kernel 3.5 % slower, profiles/r03_row_order_ab.txt.)  gridDim.x = rows * TILES * batch.
   u32 b, r, tile;
-  if ((rows * H::TILES) % 8 == 0) {
+  if (H::TILES % 8 == 0) {
     const u32 xcd = blockIdx.x % 8, k8 = blockIdx.x / 8;
-    const u32 rt = xcd + 8 * (k8 / batch);
-    b = k8 % batch;
-    r = rt % rows;
-    tile = rt / rows;
+    constexpr u32 T8 = H::TILES / 8;
+    tile = xcd + 8 * (k8 % T8);
+    const u32 rb = k8 / T8;
+    b = rb % batch;
+    r = rb / batch;
   } else {  // small N: too few tiles to deal out by XCD
     r = blockIdx.x % rows;
     b = (blockIdx.x / rows) % batch;
