@@ -889,8 +889,9 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
   xcd_limb_split(blockIdx.x, nlimbs, gridDim.x / nlimbs, l, rest);
   // tile fastest: an XCD's workgroups stream each poly-limb's rows front to back (DRAM page
   // locality; the limb's row twiddles stay in that XCD's L2 either way).  Measured against
-  // ciphertext fastest: hm_row_tensor 0.684 -> 0.668 ms, standalone row passes -8 %
-  // (profiles/r03_row_order_ab.txt)
+  // ciphertext fastest: hm_row_tensor 0.684 -> 0.668 ms, standalone row passes -8 %; against all
+  // 8 XCDs sweeping one poly-limb together (tile t on XCD t mod 8): -0.8 % on this kernel, row
+  // passes +1-4 %, the N = 2^17 row pass +15 % (profiles/r03_row_order_ab.txt)
   const u32 b = rest / H::TILES, tile = rest % H::TILES;
   const u32 limb = limb0 + l;
   const ModParams m = mods[limb];
