@@ -1066,6 +1066,9 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   const u32 blk = blockIdx.x - dg.blk0;
   const u32 nbt = batch * G::TILES_C;
   u32 tr, bt;
+  // (Tile-major per XCD instead, as k_ntt_col's placement -- a (target, ciphertext) pair's 16
+  // tiles back to back on one XCD, the sources then read by every XCD: ModUp 0.252 -> 0.277 ms,
+  // profiles/r03_row_order_ab.txt)
   if (nbt % 8 == 0) {  // every digit's block range then starts at a multiple of 8
     const u32 xcd = blk % 8, k8 = blk / 8;
     tr = k8 % T;
