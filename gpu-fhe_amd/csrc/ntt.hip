@@ -765,7 +765,9 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 
   // poly-limbs pl = x mod 8 and runs all TILES_C column tiles of one back to back.  Adjacent
   // 128-byte row segments then come from one XCD close together in time (DRAM page locality):
   // tools/microbench/colcopy.hip, this access pattern 5.30 -> 5.85 TB/s; with 8 | nlimbs the limb
-  // (and its twiddles) is also tied to the XCD.  Otherwise tiles fastest over all XCDs.
+  // (and its twiddles) is also tied to the XCD.  Otherwise tiles fastest over all XCDs.  (All 8
+  // XCDs sweeping one poly-limb's tiles together instead: HomMult column forward +3.4 %, column
+  // inverse +2.4 %, configs[4] column pass +6 %; profiles/r03_row_order_ab.txt.)
   u32 tile, pl;
   if ((items / G::TILES_C) % 8 == 0) {
     const u32 k = it / 8;
