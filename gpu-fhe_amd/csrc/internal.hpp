@@ -79,6 +79,9 @@ struct fhe_ctx {
   // Digit j covers Q-limbs [j * alpha, min(L, (j + 1) * alpha)).
   ulonglong2* d_modup_inv = nullptr;    // [dnum][alpha]        (D^_k)^-1 mod q_k
   ulonglong2* d_modup_hat = nullptr;    // [dnum][alpha][L + K] D^_k mod t  (by ctx limb t)
+  // the same with .y = D^_k 2^128 mod t: the fused lz16 ModUp's Montgomery conversion then emits
+  // the extended rows times R = 2^64, so k_ks_row_inner's inner product reduces by one REDC
+  ulonglong2* d_modup_hat_r = nullptr;  // [dnum][alpha][L + K]
   ulonglong2* d_moddown_inv = nullptr;  // [K]                  (P^_k)^-1 mod p_k
   ulonglong2* d_moddown_hat = nullptr;  // [K][L + K]           P^_k mod q_i
   ulonglong2* d_pinv = nullptr;         // [L]                  P^-1 mod q_i
@@ -131,6 +134,10 @@ struct KsRowArgs {
   const u64* evk_b;
   const u64* evk_a;
   u32 rows, nq, base0, base1, alpha, L, batch;
+  // ext rows carry a factor R = 2^64 (the fused lz16 ModUp with d_modup_hat_r): the inner product
+  // takes the own digit's d2 rows times R as well and reduces each 128-bit sum by one Montgomery
+  // REDC (R^-1) instead of reduce128
+  bool mont = false;
 };
 int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s);
 // ModUp column pass (ntt.hip, k_modup_col): converts a digit's S pre-scaled source rows

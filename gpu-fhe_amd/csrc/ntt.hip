@@ -1236,7 +1236,11 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
 // all digits publish to LDS slot j; then every thread combines 4 of its 16 positions for both
 // outputs: acc{0,1} = sum_j x_j * evk{b,a}[j][r] (128-bit sums of DNUM products, one reduce128).
 // Rows: r < nq -> own Q-limb base0 + r, else special limb base1 + (r - nq).
-template <int LOGN, int HR, int DNUM>
+// MONT (lz16 only): the ext rows arrive times R = 2^64 (k_modup_col with d_modup_hat_r), the own
+// digit's d2 rows are taken times R here (by its otherwise idle wave), and each output is one
+// subtractive REDC of the 128-bit sum (R^-1 cancels the factor) plus one subtraction, instead of
+// reduce128's two Shoup products and three subtractions.
+template <int LOGN, int HR, int DNUM, bool MONT = false>
 __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
                                          const u64* __restrict__ ext, u64 ext_ds,
                                          const u64* __restrict__ d2_own,
@@ -1291,6 +1295,13 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
       // d2 is already in NTT form: straight into the LDS slot, read in linear order
       const GView<1> gin{const_cast<u64*>(d2_own) + ((u64)b * nq + r) * N + loc, 0};
       gin.template load_lin<H::TPS>(v, t);
+      if constexpr (MONT) {
+        // v R mod q into [0, 2q) (Shoup by R mod q: [0, 3q), one subtraction): the inner
+        // product's operands must stay below 2^61
+        const u64 nq = 0 - q;
+#pragma unroll
+        for (int j = 0; j < kE; ++j) v[j] = csubk(shoup_q3(v[j], m.r64, m.r64s, nq), q);
+      }
 #pragma unroll
       for (int jj = 0; jj < kE / 2; ++jj) {
         const u32 p = 2 * t + 2 * H::TPS * jj;
@@ -1337,6 +1348,8 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
   const u64 okey = (u64)r * N + (u64)(tile * H::ROWS + crow) * G::R2 + cpos;
   const u64* lrow = lds + crow * H::ROWW;
   u64 o0[CW], o1[CW];
+  u64 qi = 0 - m.qinv;  // q^-1 mod 2^64 (MONT)
+  asm("" : "+s"(qi));
   if constexpr (HR == 16) {
 #pragma unroll
     for (int e = 0; e < CW; e += 2) {
@@ -1354,14 +1367,26 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
         ka1[d] = ka.y;
       }
       u64 tl, th;
-      dot_wide61<DNUM>(x0, kb0, tl, th);
-      o0[e] = reduce128(tl, th, m);
-      dot_wide61<DNUM>(x1, kb1, tl, th);
-      o0[e + 1] = reduce128(tl, th, m);
-      dot_wide61<DNUM>(x0, ka0, tl, th);
-      o1[e] = reduce128(tl, th, m);
-      dot_wide61<DNUM>(x1, ka1, tl, th);
-      o1[e + 1] = reduce128(tl, th, m);
+      if constexpr (MONT) {
+        // sum < DNUM 2q q <= 8 q^2 < q 2^64: REDC into (0, 2q), then canonical
+        dot_wide61<DNUM>(x0, kb0, tl, th);
+        o0[e] = csubk(mont_redc_x(tl, th, q, qi), q);
+        dot_wide61<DNUM>(x1, kb1, tl, th);
+        o0[e + 1] = csubk(mont_redc_x(tl, th, q, qi), q);
+        dot_wide61<DNUM>(x0, ka0, tl, th);
+        o1[e] = csubk(mont_redc_x(tl, th, q, qi), q);
+        dot_wide61<DNUM>(x1, ka1, tl, th);
+        o1[e + 1] = csubk(mont_redc_x(tl, th, q, qi), q);
+      } else {
+        dot_wide61<DNUM>(x0, kb0, tl, th);
+        o0[e] = reduce128(tl, th, m);
+        dot_wide61<DNUM>(x1, kb1, tl, th);
+        o0[e + 1] = reduce128(tl, th, m);
+        dot_wide61<DNUM>(x0, ka0, tl, th);
+        o1[e] = reduce128(tl, th, m);
+        dot_wide61<DNUM>(x1, ka1, tl, th);
+        o1[e + 1] = reduce128(tl, th, m);
+      }
     }
   } else {
 #pragma unroll
@@ -1599,9 +1624,14 @@ int ks_row_inner_dispatch(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
   switch (c->dnum) {
 #define D(k)                                                                                    \
   case k:                                                                                       \
-    k_ks_row_inner<LOGN, HD, k><<<g, H::THR, 0, s>>>(                                           \
-        a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.base0,   \
-        a.base1, a.alpha, a.L, a.batch, c->d_tw_fwd, c->d_mods);                               \
+    if (HD == 16 && a.mont)                                                                     \
+      k_ks_row_inner<LOGN, HD, k, HD == 16><<<g, H::THR, 0, s>>>(                               \
+          a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.base0, \
+          a.base1, a.alpha, a.L, a.batch, c->d_tw_fwd, c->d_mods);                             \
+    else                                                                                        \
+      k_ks_row_inner<LOGN, HD, k><<<g, H::THR, 0, s>>>(                                         \
+          a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.base0, \
+          a.base1, a.alpha, a.L, a.batch, c->d_tw_fwd, c->d_mods);                             \
     break;
     D(1) D(2) D(3) D(4)
 #undef D

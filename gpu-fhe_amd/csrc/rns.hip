@@ -327,6 +327,12 @@ int build_rns_tables(fhe_ctx* c) {
     std::copy(inv.begin(), inv.end(), up_inv.begin() + (size_t)j * alpha);
     std::copy(hat.begin(), hat.end(), up_hat.begin() + (size_t)j * alpha * M);
   }
+  // Montgomery-scaled copy for the fused lz16 ModUp: .y = D^_k 2^128 mod t
+  std::vector<Pair64> up_hat_r(up_hat);
+  for (size_t i = 0; i < up_hat.size(); ++i) {
+    const u64 t = c->moduli[i % M];
+    up_hat_r[i].y = (u64)(((u128)up_hat[i].y << 64) % t);
+  }
   std::vector<Pair64> dn_inv, dn_hat, pinv(L);
   conv_tables(c->moduli, L, K, dn_inv, dn_hat);
   for (u32 i = 0; i < L; ++i) {
@@ -356,6 +362,7 @@ int build_rns_tables(fhe_ctx* c) {
   }
   int rc;
   if ((rc = upload(&c->d_modup_inv, up_inv)) || (rc = upload(&c->d_modup_hat, up_hat)) ||
+      (rc = upload(&c->d_modup_hat_r, up_hat_r)) ||
       (rc = upload(&c->d_moddown_inv, dn_inv)) || (rc = upload(&c->d_moddown_hat, dn_hat)) ||
       (rc = upload(&c->d_pinv, pinv)) || (rc = upload(&c->d_nfold_down, nf_down)) ||
       (rc = upload(&c->d_nfold_up, nf_up)))
@@ -418,6 +425,9 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
   // digit's source rows; the extended rows are never written in coefficient form.
   const bool fused_up = fused && alpha <= 4;
+  // lz16 fused ModUp: the extended rows come out times R = 2^64 (d_modup_hat_r), which the fused
+  // row kernel's Montgomery inner product cancels (KsRowArgs::mont)
+  const bool mont_ext = fused_up && c->lz16;
   if (call.scaled && !fused_up) {
     set_error("keyswitch: a prepared (pre-scaled) input needs the fused ModUp (ks_prepared)");
     return kInvalid;
@@ -472,7 +482,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
       const u32 skip_at = skip_len ? own_lo - limb0 : rows;
       const ModUpColArgs ma{ysrc, ybs, {yoff[0], yoff[1], yoff[2], yoff[3]}, e, rn, S,
                             rows - skip_len, skip_at, skip_len, nlimbs, limb0, L, batch,
-                            c->d_modup_hat + (size_t)j * alpha * M, M};
+                            (mont_ext ? c->d_modup_hat_r : c->d_modup_hat) + (size_t)j * alpha * M,
+                            M};
       if (call.scaled && npend < 4) {
         pend[npend++] = ma;
         continue;
@@ -497,7 +508,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   }
   if (fused) {
     const KsRowArgs ka{acc, acc_ws, ext, B * rn, d2_own, evk_b, evk_a, rows, nlimbs, limb0, L,
-                       alpha, L, batch};
+                       alpha, L, batch, mont_ext};
     if ((rc = launch_ks_row_inner(c, ka, s))) return rc;
   }
   const dim3 gi((u32)(n / kThreads), rows);
