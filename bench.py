@@ -59,7 +59,7 @@ def parse():
                          "exact wide-modulus butterflies)")
     ap.add_argument("--ks-chunks", type=int, default=0,
                     help="keyswitch: all-gather chunks per batch (0 = 1 at N = 1, 4 above)")
-    ap.add_argument("--ks-batch", type=int, default=16,
+    ap.add_argument("--ks-batch", type=int, default=32,
                     help="keyswitch (and the default line's key-switch leg): ciphertexts per "
                          "call, the whole job's (limbs sharded: strong scaling)")
     ap.add_argument("--no-keyswitch-leg", action="store_true",
