@@ -77,10 +77,11 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
   c->lz16 = true;
   c->wide = false;
   for (u64 m : mods) {
-    // lz16: m < 2^60 and m >= 2^s - 2^(s-4), s = bitlength(m) (the forward NTT's top-bits
-    // reductions, ntt.hip top_bits); the largest primes below a power of two all qualify
+    // lz16: 2^32 < m < 2^60 and m >= 2^s - 2^(s-4), s = bitlength(m) (the top-bits reductions,
+    // ntt.hip top_bits, work on the 32-bit halves); the largest primes below a power of two all
+    // qualify
     const u64 pw = 1ull << (63 - __builtin_clzll(m));  // 2^(s-1)
-    c->lz16 = c->lz16 && m < (1ull << 60) && m >= 16 && m >= 2 * pw - pw / 8;
+    c->lz16 = c->lz16 && m < (1ull << 60) && m > (1ull << 32) && m >= 2 * pw - pw / 8;
     c->wide = c->wide || m >= (1ull << 61);
   }
   c->log_n = log_n;

@@ -148,18 +148,40 @@ def test_folded_ct_butterfly(q, H):
 
 
 def top_bits(x, q):
-    """ntt.hip top_bits: x + (x >> s) (-q) mod 2^64, s = bitlength(q)."""
+    """ntt.hip top_bits on 32-bit halves: (x mod 2^s) + k c, k = x >> s, c = 2^s - q = -q + 2^s
+    mod 2^64 (s = bitlength(q)): one 32 x 32 + 64 mad for k c_lo into {lo x, masked hi x}, and
+    k c_hi by a 24-bit mad into the high word.  Checks the operand bounds those instructions
+    need and that the value equals x + k (-q) mod 2^64 (the previous form)."""
     s = q.bit_length()
-    return (x + ((x >> s) & M32) * ((-q) & M64)) & M64
+    assert 33 <= s <= 60
+    c = ((-q) + (1 << s)) & M64
+    c0, c1 = c & M32, c >> 32
+    hi = x >> 32
+    k = hi >> (s - 32)
+    hm = hi & ((1 << (s - 32)) - 1)
+    assert k < 16 and c1 < 1 << 24  # v_mad_u32_u24 operands
+    r = k * c0 + ((hm << 32) | (x & M32))
+    assert r < 1 << 64  # v_mad_u64_u32 does not wrap
+    hi_out = (k * c1 + (r >> 32)) & M32
+    out = (hi_out << 32) | (r & M32)
+    assert out == (x + ((x >> s) & M32) * ((-q) & M64)) & M64
+    return out
 
 
 def _lz16(q):
-    """context.cpp: q < 2^60 within 1/16 below a power of two."""
+    """context.cpp: 2^32 < q < 2^60, within 1/16 below a power of two."""
     s = q.bit_length()
-    return q < 1 << 60 and q >= (1 << s) - (1 << (s - 4))
+    return 1 << 32 < q < 1 << 60 and q >= (1 << s) - (1 << (s - 4))
 
 
-@pytest.mark.parametrize("bits", [20, 31, 32, 33, 40, 50, 55, 59, 60])
+def test_lz16_excludes_small_moduli():
+    """top_bits works on the 32-bit halves, so moduli up to 2^32 take the H = 8 kernels."""
+    for bits in (20, 31, 32):
+        for q in pyoracle.gen_moduli(10, 2, bits=bits):
+            assert not _lz16(q)
+
+
+@pytest.mark.parametrize("bits", [33, 34, 40, 50, 55, 59, 60])
 def test_top_bits_reduction(bits):
     """For every lz16 modulus and x < 16 q: top_bits(x) < 2q, congruent to x (the forward CT
     reductions and the final forward reduction of H = 16 kernels)."""
