@@ -64,7 +64,10 @@ def _prime_below(bound):
     return q
 
 
-CHAINS = ["b50", "b55", "b60", "b61", "b62", "b63", "mixed-wide", "mixed-narrow", "far"]
+# b33 / b34: the smallest lz16 moduli (top_bits works on the 32-bit halves, shift s - 32 = 1, 2);
+# b32: below 2^32, so the context takes the 8q kernels
+CHAINS = ["b32", "b33", "b34", "b50", "b55", "b60", "b61", "b62", "b63", "mixed-wide",
+          "mixed-narrow", "far"]
 _CTX = {}
 
 
@@ -75,12 +78,24 @@ def ctx_for(fc, name):
     return _CTX[name]
 
 
+@pytest.mark.parametrize("name,lz16", [("b32", False), ("b33", True), ("b34", True), ("b60", True),
+                                       ("far", False)])
+def test_chain_width_class(fc, name, lz16):
+    """The chains above reach the kernel family they are meant to (fhe_ctx::lz16: every modulus
+    in (2^32, 2^60) within 1/16 below a power of two)."""
+    qs, ps = _chain(fc, name)
+    in_class = all((1 << 32) < q < (1 << 60) and q >= (1 << q.bit_length()) - (1 << (q.bit_length() - 4))
+                   for q in qs + ps)
+    assert in_class == lz16
+
+
 @pytest.mark.parametrize("name", CHAINS)
 def test_chain_ntt_and_hommult(fc, name):
     ctx = ctx_for(fc, name)
     qs = ctx.moduli
     top = max(ctx.all_moduli).bit_length()
-    assert top == {"b50": 50, "b55": 55, "b60": 60, "b61": 61, "b62": 62, "b63": 63,
+    assert top == {"b32": 32, "b33": 33, "b34": 34, "b50": 50, "b55": 55, "b60": 60, "b61": 61,
+                   "b62": 62, "b63": 63,
                    "mixed-wide": 63, "mixed-narrow": 60, "far": 59}[name]
     x = rand(qs, LOG_N, (3,), seed=1)
     t = fc.to_device(x)
