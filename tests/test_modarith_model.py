@@ -417,6 +417,42 @@ def test_keyswitch_inner_product_dot(q):
             assert dot_wide61(xs, ks) == sum(x * k for x, k in zip(xs, ks))
 
 
+@pytest.mark.parametrize("q", [q for q in _moduli() if _lz16(q)])
+def test_keyswitch_montgomery_inner_product(q):
+    """k_ks_row_inner<..., MONT>: the extended rows arrive times R = 2^64 (ModUp converted with
+    D^_k 2^128 mod t), the own digit's canonical d2 row is taken times R by Shoup (shoup_q3 with
+    {2^64 mod q, its companion}: [0, 3q)) and one subtraction into [0, 2q); the 128-bit sum of D <= 4
+    products (< 8 q^2 < q 2^64) is reduced by mont_redc_x and one subtraction.  The output must equal
+    the canonical sum of the unscaled products, so the result is bit-identical to reduce128's."""
+    rng = random.Random(q + 13)
+    R = 1 << 64
+    r64 = R % q
+    r64s = (r64 << 64) // q
+    for D in (1, 2, 3, 4):
+        for trial in range(1500):
+            xs = [rng.randrange(q) for _ in range(D)]  # canonical NTT-form digit values
+            ks = [rng.randrange(q) for _ in range(D)]
+            if trial == 0:
+                xs, ks = [q - 1] * D, [q - 1] * D
+            own = rng.randrange(D)
+            ops = []
+            for d, x in enumerate(xs):
+                if d == own:  # d2 row: scaled in the kernel
+                    y = shoup_q3(x, r64, r64s, q)
+                    assert y < 3 * q and y % q == x * R % q
+                    y = y - q if y >= q else y
+                else:  # ext row: ModUp emitted x R mod q, the row NTT leaves it in [0, 2q)
+                    y = x * R % q + rng.choice((0, q))
+                assert y < 2 * q and y < 1 << 61
+                ops.append(y)
+            t = dot_wide61(ops, ks)
+            assert t == sum(y * k for y, k in zip(ops, ks)) and t < q << 64
+            r = mont_redc_x(t, q)
+            assert 0 < r < 2 * q
+            r = r - q if r >= q else r
+            assert r == sum(x * k for x, k in zip(xs, ks)) % q
+
+
 def gs_red(r):
     return 2 if r > 8 else r
 
