@@ -299,7 +299,7 @@ constexpr int gs_in(int j, int k) {
 // ROWTAB: the twiddles come from a row table region (base = R1 + row), whose low-bit-round stages
 // are stored lane-major.
 template <int LOGR, int KB, int LO, bool FWD, int FIN, bool GATHER = false, int H = 8,
-          int RIN = 8, bool ROWTAB = GATHER>
+          int RIN = 8, bool ROWTAB = GATHER, bool CHAIN = GATHER>
 __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
                                               const ulonglong2* __restrict__ tw, const u32 base,
                                               const u64 q, const ulonglong2 nf0,
@@ -380,7 +380,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         if constexpr (reduce) u = H == 16 ? top_bits(u, sb, nq) : csubk(u, qh);
         FHE_OPAQUE(u);  // keeps 2u + 3q one v_lshl_add_u64 (not distributed over the select)
         // u + v straight out of the remainder chain; u - v + 3q = (2u + 3q) - (u + v)
-        u64 s = shoup_q3_add<GATHER>(x[jj], w.x, w.y, nq, u);
+        u64 s = shoup_q3_add<CHAIN>(x[jj], w.x, w.y, nq, u);
         FHE_OPAQUE(s);
         x[j] = s;
         u64 t2 = (u << 1) + q3;
@@ -469,7 +469,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
           } else {
             const ulonglong2 w = twiddle(b, j, bitpos, st);
             x[j] = sum;
-            x[jj] = shoup_q3<GATHER>(dif, w.x, w.y, nq);
+            x[jj] = shoup_q3<CHAIN>(dif, w.x, w.y, nq);
           }
         }
       });
@@ -662,7 +662,7 @@ __device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
 // straight from registers, whose last-round positions are E consecutive words per thread, so a
 // direct store instruction writes 16 of every 16 E bytes across 16 E * 64 bytes.
 template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, int H, int R0, bool XOUT = false,
-          class GOut, class LV>
+          bool CHAIN = GATHER, class GOut, class LV>
 __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const LV& lv, u32 t,
                                          const ulonglong2* __restrict__ tw, u32 base, u64 q,
                                          ulonglong2 nf0, ulonglong2 nf1) {
@@ -684,7 +684,7 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     // column pass's few shared twiddles are left to the scheduler
     const ulonglong2* twk = tw;
     if constexpr (GATHER) asm volatile("" : "+s"(twk));
-    round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN>(x, tp, twk, base, q, nf0, nf1);
+    round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN, GATHER, CHAIN>(x, tp, twk, base, q, nf0, nf1);
     if constexpr (k == Rd::NR - 1) {
       if constexpr (XOUT) {
         constexpr u32 TPS = (1u << LOGR) / kE;
@@ -1137,7 +1137,10 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
       x[j] = acc.mont_lazy(m.q, m.qinv);  // [0, 2q): the pass takes inputs below 2q
     }
   }
-  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2>(
+  // mad-chain remainders (CHAIN) although this is a column pass: unlike the latency-bound column
+  // passes of the NTTs, this one is VALU-bound (the conversion products): ModUp -1.1 %, ModDown
+  // conversion pass -1 % same-box (profiles/r03_modup_chain_ab.txt)
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2, false, true>(
       x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
       tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
 }
