@@ -38,6 +38,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--ks-batch", type=int, default=32, help="the key-switch leg's batch (bench.py)")
     args = ap.parse_args()
     log_n, n, L = 16, 1 << 16, 8
     ctx = fc.Context(log_n, L=L)
@@ -70,10 +71,10 @@ def main():
                          "per_gpu_ntt_per_s": round(2 * npolys * sh.nlimbs / dn, 1)}
         del a, b, d, ws, x
         torch.cuda.empty_cache()
-    # key-switch leg, rank 0 of N: its limb shard of the batch of 16 over a ranked gather region
+    # key-switch leg, rank 0 of N: its limb shard of the leg's batch over a ranked gather region
     # filled with residues (timing only: the per-rank kernels of fhe_keyswitch_dist after its
     # gather)
-    Lk, K, dnum, B = 16, 4, 4, 16
+    Lk, K, dnum, B = 16, 4, 4, args.ks_batch
     kctx = fc.Context(log_n, L=Lk, K=K, dnum=dnum)
     lib = load()
     for G in (1, 2, 4, 8):
@@ -97,12 +98,12 @@ def main():
             assert rc == 0, lib.fhe_last_error()
 
         dk = rate(ks, 20, 50)
-        out[f"ks N={G}"] = {"limbs_per_gpu": sh.nlimbs, "ms_per_batch_of_16": round(dk * 1e3, 4),
+        out[f"ks N={G}"] = {"limbs_per_gpu": sh.nlimbs, "batch": B, "ms_per_batch": round(dk * 1e3, 4),
                             "speedup_vs_N1_if_gather_hidden": None}
-    base = out["ks N=1"]["ms_per_batch_of_16"]
+    base = out["ks N=1"]["ms_per_batch"]
     for G in (1, 2, 4, 8):
         out[f"ks N={G}"]["speedup_vs_N1_if_gather_hidden"] = round(
-            base / out[f"ks N={G}"]["ms_per_batch_of_16"], 3)
+            base / out[f"ks N={G}"]["ms_per_batch"], 3)
     print(json.dumps(out, indent=1))
 
 
