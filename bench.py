@@ -66,6 +66,9 @@ def parse():
                     help="hommult: skip the key-switch ride-along leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="hommult: skip the live rocprofv3 traffic passes (roofline.traffic then "
+                         "falls back to the committed profiles/hbm_traffic.json)")
     return ap.parse_args()
 
 
@@ -213,6 +216,57 @@ def traffic_from_profile(kernel, shape):
                                      "and per-GPU shape")
 
 
+def measure_traffic_live(kernel_match, probe_args, timeout_s=150):
+    """HBM bytes per launch of the kernel whose name contains `kernel_match`, measured in this run:
+    two rocprofv3 passes (--pmc FETCH_SIZE, then --pmc WRITE_SIZE, one counter group each, no
+    tracing) over a child process that repeats the launch at the bench shape
+    (tools/hm_traffic_probe.py), corrected as MI355X_MICROARCH.md's HBM section prescribes and as
+    tools/pmc_traffic.sh calibrated on the column pass: read = 2 x FETCH_SIZE KiB, write =
+    WRITE_SIZE KiB.  The child is started as a new process (never exec), in its own session, and
+    killed with its group on timeout.  Returns (bytes, None) or (None, reason)."""
+    import csv
+    import glob
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    tmp = tempfile.mkdtemp(prefix="fhe_pmc_", dir="/tmp")
+    per = {}
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.join(ROOT, "tools", "hm_traffic_probe.py"), *probe_args]
+            env = dict(os.environ, TMPDIR="/tmp")
+            proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+                                    stderr=subprocess.DEVNULL, start_new_session=True)
+            try:
+                rc = proc.wait(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(proc.pid, signal.SIGKILL)
+                proc.wait()
+                return None, f"rocprofv3 --pmc {counter} timed out after {timeout_s} s"
+            if rc != 0:
+                return None, f"rocprofv3 --pmc {counter} exited with {rc}"
+            vals = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for r in csv.DictReader(fh):
+                        if kernel_match in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                            vals.append(float(r["Counter_Value"]))
+            if not vals:
+                return None, f"no {kernel_match} dispatch in the {counter} pass"
+            per[counter] = sum(vals) / len(vals)
+    except (OSError, ValueError, KeyError) as e:
+        return None, f"traffic measurement failed: {e}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return int(2 * 1024 * per["FETCH_SIZE"] + 1024 * per["WRITE_SIZE"]), None
+
+
 def roofline(kernel, alg_bytes, ms, shape):
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     traffic, src = traffic_from_profile(kernel, shape)
@@ -344,6 +398,21 @@ def run_hommult(args, world, rank):
         out["roofline"]["frac"] else "hbm"
     if args.bits != 60:
         out["config"]["modulus_bits"] = args.bits
+    # HBM traffic of the dominant kernel measured in this run (rank 0 of a one-GPU job only: the
+    # profiled child shares the GPU); the committed figure stays beside it for comparison
+    if rank == 0 and world == 1 and not args.no_pmc and args.bits == 60:
+        live, why = measure_traffic_live("k_hommult_row", [
+            "--log-n", str(args.log_n), "--limbs", str(L), "--batch", str(gbatch)])
+        rf = out["roofline"]
+        if live is not None:
+            rf["traffic_committed"], rf["traffic"] = rf["traffic"], live
+            rf["traffic_source"] = (
+                "measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes "
+                "(separate) over tools/hm_traffic_probe.py at this shape, k_hommult_row mean per "
+                "dispatch; read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB (gfx950 correction)")
+            rf["traffic_over_alg"] = round(live / alg, 4)
+        else:
+            rf["traffic_live_error"] = why
     if not (args.no_keyswitch_leg or args.bits != 60):
         out["keyswitch_leg"] = guarded_leg(
             lambda: KeyswitchLeg(args, world, rank).run(argparse.Namespace(warmup=20, steps=50)),

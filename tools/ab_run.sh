@@ -10,7 +10,7 @@ tail -2 "$out/gputests.log"
 bash tools/ab_bench.sh "$out/ab.txt" "$reps" "$args" default "$@" || exit $?
 cat "$out/ab.txt"
 if [ -n "$targs" ]; then
-  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$out/kt" -o kt -- python3 bench.py --no-cpu-baseline $targs > "$out/trace_line.json" 2> "$out/trace.err" || exit $?
+  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$out/kt" -o kt -- python3 bench.py --no-cpu-baseline --no-pmc $targs > "$out/trace_line.json" 2> "$out/trace.err" || exit $?
   f=$(find "$out/kt" -name '*kernel_trace.csv' | head -1)
   python3 tools/trace_gaps.py "$f" --last 600 > "$out/gaps.txt" && cat "$out/gaps.txt"
 fi
