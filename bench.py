@@ -230,7 +230,8 @@ def measure_traffic_live(kernel_match, probe_args, timeout_s=150):
     import signal
     import subprocess
     import tempfile
-    prof = shutil.which("rocprofv3")
+    prof = shutil.which("rocprofv3") or (
+        "/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
     if not prof:
         return None, "rocprofv3 not found"
     tmp = tempfile.mkdtemp(prefix="fhe_pmc_", dir="/tmp")
