@@ -166,8 +166,14 @@ def cpu_threads():
 def cpu_host():
     """What the cpu_baseline ran on: the model, the threads used, the CPUs this process may use
     (sched_getaffinity) and the machine's total (os.cpu_count: the whole box, shared)."""
+    omp = os.environ.get("OMP_NUM_THREADS")
+    why = (f"OMP_NUM_THREADS={omp} is set by the GPU box, which allots that many host CPUs to "
+           "each GPU; the affinity mask and cpu_count show the whole shared machine, so using them "
+           "would time CPUs allotted to other jobs" if omp else
+           "OMP_NUM_THREADS unset: every CPU of the affinity mask")
     return {"cpu_model": cpu_model(), "threads": cpu_threads(),
-            "affinity_cpus": len(os.sched_getaffinity(0)), "host_cpus": os.cpu_count()}
+            "affinity_cpus": len(os.sched_getaffinity(0)), "host_cpus": os.cpu_count(),
+            "threads_why": why}
 
 
 def cpu_baseline_hommult(moduli, log_n, budget_s):
@@ -414,10 +420,17 @@ def run_hommult(args, world, rank):
             rf["traffic_over_alg"] = round(live / alg, 4)
         else:
             rf["traffic_live_error"] = why
+    legs = {}
     if not (args.no_keyswitch_leg or args.bits != 60):
-        out["keyswitch_leg"] = guarded_leg(
-            lambda: KeyswitchLeg(args, world, rank).run(argparse.Namespace(warmup=20, steps=50)),
-            out, rank, "keyswitch_leg")
+        def ks_leg():
+            legs["ks"] = KeyswitchLeg(args, world, rank)
+            return legs["ks"].run(argparse.Namespace(warmup=20, steps=50))
+
+        out["keyswitch_leg"] = guarded_leg(ks_leg, out, rank, "keyswitch_leg")
+    # after every timed leg: the sharded paths against each rank's single-device result
+    out["dist_check"] = guarded_leg(lambda: dist_check(world, rank, hm_ctx=ctx,
+                                                       ks_leg=legs.get("ks")),
+                                    out, rank, "dist_check")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_hommult(ctx.moduli, args.log_n, args.cpu_seconds)
@@ -770,6 +783,8 @@ def run_keyswitch(args, world, rank):
     out.pop("warmup")
     out.pop("steps")
     out["scaling"] = out["config"].pop("scaling")
+    out["dist_check"] = guarded_leg(lambda: dist_check(world, rank, ks_leg=leg), out, rank,
+                                    "dist_check")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_keyswitch(leg.ctx.moduli, leg.ctx.special, args.log_n, leg.DNUM,
@@ -957,11 +972,113 @@ def cpu_baseline_rotate(moduli, special, log_n, dnum, budget_s):
                       f"key-switch, OpenMP {cpu_threads()} threads, in {dt:.1f} s"}
 
 
-_EMIT = {}  # json_fd, args, world: what emit_line needs (set by main)
+def shard_mismatches(got, ref_full, shard) -> int:
+    """Words of this rank's limb slice `got` [..., nlimbs, N] that differ from its limbs of the
+    single-device result `ref_full` [..., L, N]."""
+    if shard.nlimbs == 0:
+        return 0
+    return int((got != shard.own(ref_full)).sum().item())
+
+
+def check_keyswitch_shard(engine, shard, K, d2, evk_b, evk_a, dist_fn) -> int:
+    """One rank's bitwise check of the limb-sharded key-switch (G ranks must equal
+    G = 1 bit for bit).  Every rank holds the same full seeded d2 [B, L, N] and key [dnum, L + K,
+    N]; it runs the distributed path on its own slices (dist_fn(d2_own, evk_b_own, evk_a_own) ->
+    (ks0_own, ks1_own), a collective every rank enters) and the single-device key-switch of the
+    whole input on its own device, and counts the mismatched words of its own limbs."""
+    rows = shard.evk_rows(K)
+    k0, k1 = dist_fn(shard.own(d2).contiguous(), evk_b[:, rows].contiguous(),
+                     evk_a[:, rows].contiguous())
+    r0, r1 = engine.keyswitch(d2, evk_b, evk_a)
+    return shard_mismatches(k0, r0, shard) + shard_mismatches(k1, r1, shard)
+
+
+def check_hommult_shard(engine, shard, a, b) -> int:
+    """The same for the limb-sharded HomMult: a, b [B, 2, L, N] full on every rank."""
+    got = fdist.sharded_hommult(engine, shard.own(a).contiguous(), shard.own(b).contiguous(), shard)
+    return shard_mismatches(got, engine.hommult(a, b), shard)
+
+
+def sum_over_ranks(x: int, world: int) -> int:
+    if world == 1:
+        return x
+    nccl = torch.distributed.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.int64, device="cuda" if nccl else "cpu")
+    torch.distributed.all_reduce(t)
+    return int(t.item())
+
+
+def dist_check(world, rank, hm_ctx=None, ks_leg=None, seed=4321):
+    """Bitwise check of the multi-GPU paths this process timed, outside every timed window: the
+    native RCCL key-switch (fhe_keyswitch_dist, chunked like the leg) and one limb-sharded HomMult
+    batch against each rank's single-device result (fhe_keyswitch / fhe_hommult of the full
+    input).  The inputs come from one seed shared by all ranks, so every rank can rebuild the whole
+    ciphertext.  Returns "bit-exact" or {"mismatched_words": n, ...} summed over the ranks."""
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(seed)
+    parts, bad = [], 0
+    if hm_ctx is not None:
+        shard = fdist.LimbShard(hm_ctx.L, world, rank)
+        a = uniform_limbs(gen, hm_ctx.moduli, (2, 2), hm_ctx.n)
+        b = uniform_limbs(gen, hm_ctx.moduli, (2, 2), hm_ctx.n)
+        bad += check_hommult_shard(hm_ctx, shard, a, b)
+        parts.append(f"sharded HomMult (2 ciphertexts, L={hm_ctx.L})")
+        del a, b
+    if ks_leg is not None:
+        ctx, shard = ks_leg.ctx, ks_leg.shard
+        # a batch of 2 per chunk so that the chunked own-stream path (chunks > 1) runs as timed
+        B = 2 * ks_leg.chunks
+        d2 = uniform_limbs(gen, ctx.moduli, (B,), ctx.n)
+        kb = uniform_limbs(gen, ctx.all_moduli, (ks_leg.DNUM,), ctx.n)
+        ka = uniform_limbs(gen, ctx.all_moduli, (ks_leg.DNUM,), ctx.n)
+        if ks_leg.native:
+            fn = lambda d, eb, ea: ctx.keyswitch_dist(ks_leg.comm, d, eb, ea,  # noqa: E731
+                                                      chunks=ks_leg.chunks)
+            how = f"fhe_keyswitch_dist over RCCL, {ks_leg.chunks} chunk(s)"
+        else:
+            fn = lambda d, eb, ea: fdist.sharded_keyswitch(ctx, d, eb, ea, shard)  # noqa: E731
+            how = "torch.distributed all_gather form (gloo)"
+        bad += check_keyswitch_shard(ctx, shard, ks_leg.K, d2, kb, ka, fn)
+        parts.append(f"key-switch ({how}, batch {B}, L={ctx.L}, K={ctx.K})")
+        del d2, kb, ka
+    torch.cuda.synchronize()
+    bad = sum_over_ranks(bad, world)
+    what = f"{world} rank(s) vs each rank's single-device fhe_keyswitch / fhe_hommult: " + \
+        "; ".join(parts)
+    if bad == 0:
+        return {"result": "bit-exact", "checked": what}
+    return {"result": "MISMATCH", "mismatched_words": bad, "checked": what}
+
+
+_EMIT = {"failed": []}  # json_fd, args, world (set by main); failed: reasons for a non-zero exit
+_EMIT_LOCK = None
+
+
+def failure_reasons(out):
+    """Why this run must exit non-zero although its line was printed: a ride-along leg that raised
+    or never finished, or a dist_check that found mismatched words."""
+    why = list(_EMIT.get("failed", []))
+    for k, v in out.items():
+        if isinstance(v, dict) and "error" in v:
+            why.append(f"{k}: {v['error']}")
+    dc = out.get("dist_check")
+    if isinstance(dc, dict) and dc.get("result") != "bit-exact":
+        why.append(f"dist_check: {dc}")
+    return why
 
 
 def emit_line(out, cpu):
-    """Rank 0's one JSON line on the saved stdout."""
+    """Rank 0's one JSON line on the saved stdout -- at most once per process, whichever thread
+    (the main one or a leg's watchdog) gets there first."""
+    global _EMIT_LOCK
+    import threading
+
+    if _EMIT_LOCK is None:
+        _EMIT_LOCK = threading.Lock()
+    with _EMIT_LOCK:
+        if _EMIT.get("emitted"):
+            return False
+        _EMIT["emitted"] = True
     args, world = _EMIT["args"], _EMIT["world"]
     out = dict(out)
     line = {"metric": out.pop("metric"), "value": out.pop("value"), "unit": out.pop("unit"),
@@ -975,13 +1092,19 @@ def emit_line(out, cpu):
     line["cpu_baseline"] = cpu
     sys.stdout.flush()
     os.write(_EMIT["json_fd"], (json.dumps(line) + "\n").encode())
+    return True
+
+
+EXIT_LEG_FAILED = 3  # the line was printed, but a leg failed, hung or a dist_check mismatched
 
 
 def guarded_leg(fn, out, rank, name, timeout_s=180.0):
-    """Runs a ride-along leg after the headline is measured, so that nothing it does can cost the
-    headline line: an exception becomes {"error": ...} in the line, and a leg still running after
-    `timeout_s` (e.g. a collective that never completes on some node) makes rank 0 print the line
-    without it and every rank exit."""
+    """Runs a ride-along leg (or the dist_check) after the headline is measured, so that nothing
+    it does can cost the headline line -- but neither can it pass for a success: an exception
+    becomes {"error": ...} in the line and the process exits EXIT_LEG_FAILED after printing it
+    (main / conclude), and a leg still running after `timeout_s` (e.g. a collective that never
+    completes on some node) makes rank 0 print the line without it and every rank exit
+    EXIT_LEG_FAILED at once."""
     import threading
 
     def fire():
@@ -989,17 +1112,33 @@ def guarded_leg(fn, out, rank, name, timeout_s=180.0):
             o = dict(out)
             o[name] = {"error": f"did not finish within {timeout_s:.0f} s; line emitted without it"}
             emit_line(o, None)
-        os._exit(0)
+        sys.stderr.write(f"bench.py: {name} did not finish within {timeout_s:.0f} s\n")
+        sys.stderr.flush()
+        os._exit(EXIT_LEG_FAILED)
 
     timer = threading.Timer(timeout_s, fire)
     timer.daemon = True
     timer.start()
     try:
         return fn()
-    except Exception as e:  # noqa: BLE001 -- reported in the line, the headline stands
+    except Exception as e:  # noqa: BLE001 -- reported in the line, then a non-zero exit
+        _EMIT.setdefault("failed", []).append(f"{name}: {type(e).__name__}")
         return {"error": f"{type(e).__name__}: {e}"}
     finally:
         timer.cancel()
+
+
+def conclude(out, cpu, rank):
+    """Print rank 0's line, then the exit status of this rank: 0, or EXIT_LEG_FAILED when a leg
+    raised or hung, or the dist_check found mismatched words (every rank sees the summed count,
+    so every rank exits non-zero together)."""
+    if rank == 0:
+        emit_line(out, cpu)
+    why = failure_reasons(out)
+    if why:
+        sys.stderr.write("bench.py: exiting %d: %s\n" % (EXIT_LEG_FAILED, "; ".join(why)))
+        return EXIT_LEG_FAILED
+    return 0
 
 
 def main():
@@ -1018,10 +1157,11 @@ def main():
     run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch, "vec": run_vec,
            "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch, "rotate": run_rotate}[args.workload]
     out, cpu = run(args, world, rank)
-    if rank == 0:
-        emit_line(out, cpu)
+    rc = conclude(out, cpu, rank)
     if world > 1:
         torch.distributed.destroy_process_group()
+    if rc:
+        sys.exit(rc)
 
 
 if __name__ == "__main__":

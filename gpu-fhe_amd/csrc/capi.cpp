@@ -37,7 +37,47 @@ int check_window(const fhe_ctx* c, uint32_t limb0, uint32_t nlimbs, uint32_t lim
 // which includes the last call's launches since calls sharing the internal workspace are issued
 // one after another by the host (concurrent host threads must pass their own workspaces,
 // fhecore.h).  The last user's stream is not touched again: the caller may have destroyed it.
-// Growing the buffer waits the same way before the old one is freed.
+// Growing the buffer waits the same way before the old one is freed.  The waits, frees and
+// allocations run on the context's device whatever device the calling thread has current
+// (DeviceScope), so a multi-GPU host thread cannot wait on, or allocate from, the wrong GPU.
+// use = false (fhe_ctx_reserve) only sizes the buffer: no stream takes it.
+namespace {
+
+// Makes `dev` current for the scope and restores the caller's device after.
+struct DeviceScope {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceScope(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int acquire_ws(fhe_ctx* c, size_t bytes, hipStream_t s, bool use) {
+  DeviceScope dev(c->device);
+  FHE_HIP_CHECK(dev.err);
+  std::lock_guard<std::mutex> lock(c->ws_mutex);
+  const bool grow = c->workspace_bytes < bytes;
+  if (c->ws_used && ((use && c->ws_stream != s) || grow)) FHE_HIP_CHECK(hipDeviceSynchronize());
+  if (grow) {
+    if (c->workspace) FHE_HIP_CHECK(hipFree(c->workspace));
+    c->workspace = nullptr;
+    c->workspace_bytes = 0;
+    FHE_HIP_CHECK(hipMalloc(&c->workspace, bytes));
+    c->workspace_bytes = bytes;
+  }
+  if (use) {
+    c->ws_stream = s;
+    c->ws_used = true;
+  }
+  return kOk;
+}
+
+}  // namespace
+
 int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws, hipStream_t s) {
   if (*ws) return kOk;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -47,18 +87,8 @@ int ensure_ws(const fhe_ctx* cc, size_t bytes, void** ws, hipStream_t s) {
     return kInvalid;
   }
   auto* c = const_cast<fhe_ctx*>(cc);
-  std::lock_guard<std::mutex> lock(c->ws_mutex);
-  const bool grow = c->workspace_bytes < bytes;
-  if (c->ws_used && (c->ws_stream != s || grow)) FHE_HIP_CHECK(hipDeviceSynchronize());
-  if (grow) {
-    if (c->workspace) FHE_HIP_CHECK(hipFree(c->workspace));
-    c->workspace = nullptr;
-    c->workspace_bytes = 0;
-    FHE_HIP_CHECK(hipMalloc(&c->workspace, bytes));
-    c->workspace_bytes = bytes;
-  }
-  c->ws_stream = s;
-  c->ws_used = true;
+  int rc = acquire_ws(c, bytes, s, true);
+  if (rc) return rc;
   *ws = c->workspace;
   return kOk;
 }
@@ -130,8 +160,7 @@ int fhe_ctx_reserve(fhe_ctx* c, size_t bytes) {
     set_error("fhe_ctx_reserve: null context");
     return kInvalid;
   }
-  void* ws = nullptr;
-  return ensure_ws(c, bytes, &ws, nullptr);
+  return acquire_ws(c, bytes, nullptr, false);
 }
 
 static int vec_ctx(int op, const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint64_t* b,

@@ -37,9 +37,6 @@ namespace {
 constexpr int kElog = 4;
 constexpr int kE = 1 << kElog;
 constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per workgroup
-#ifndef FHE_INVXOUT
-#define FHE_INVXOUT 0
-#endif
 // Column-pass workgroup size: 16 columns per 256 threads at N = 2^16.  (512 threads, i.e. wider
 // tiles, measured -4 % on the N = 2^17 ntt-batch column pass and +9 % on the HomMult column
 // inverse; 256 kept everywhere.)
@@ -837,7 +834,7 @@ __device__ __forceinline__ void row_tile(u64* lds, const u64* __restrict__ src,
     pass_load<G::N2, FWD>(gin, t, x);
   }
   pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, H, fwd_range(1, G::N1, H),
-           FWD || FHE_INVXOUT>(x, GView<1, false, NTS>{dst + pm.dst(p) + loc, lane}, lv, t,
+           FWD>(x, GView<1, false, NTS>{dst + pm.dst(p) + loc, lane}, lv, t,
                 tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, mods[limb].q, {0, 0}, {0, 0});
 }
 

@@ -556,6 +556,9 @@ class Context:
         evk_* [dnum, nlimbs + K, N].  Returns (ks0, ks1) shaped like d2_own."""
         for t, nm in ((d2_own, "d2_own"), (evk_b, "evk_b"), (evk_a, "evk_a")):
             _check_tensor(t, nm, (self.n,))
+            if t.device != self._dev():
+                raise ValueError(f"keyswitch_dist: {nm} is on {t.device}, the context on "
+                                 f"{self._dev()}")
         shard = comm.shard(self.L)
         nl = d2_own.shape[-2]
         if nl != shard.nlimbs:
@@ -593,10 +596,13 @@ class Context:
                 continue
             d2 = d2_parts[r]
             _check_tensor(d2, f"d2[{r}]", (sh.nlimbs, self.n))
-            for t, nm in ((evk_b_parts[r], "evk_b"), (evk_a_parts[r], "evk_a")):
-                _check_tensor(t, f"{nm}[{r}]", (self.dnum, sh.nlimbs + self.K, self.n))
-                if t.device != d2.device:
-                    raise ValueError("keyswitch_dist_loopback: every tensor on one device")
+            for t, nm in ((d2, "d2"), (evk_b_parts[r], "evk_b"), (evk_a_parts[r], "evk_a")):
+                if nm != "d2":
+                    _check_tensor(t, f"{nm}[{r}]", (self.dnum, sh.nlimbs + self.K, self.n))
+                # the C side launches on the context's device with these raw pointers
+                if t.device != self._dev():
+                    raise ValueError(f"keyswitch_dist_loopback: {nm}[{r}] is on {t.device}, "
+                                     f"the context on {self._dev()}")
             b = d2.numel() // (sh.nlimbs * self.n)
             if batch is not None and b != batch:
                 raise ValueError("keyswitch_dist_loopback: every rank needs the same batch")

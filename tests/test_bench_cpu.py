@@ -1,39 +1,168 @@
-"""CPU checks of bench.py's ride-along guard (no GPU): a failing key-switch leg is reported inside
-the line, and a leg that never finishes makes rank 0 print the line without it and exit -- so the
-driver's scaling runs always get the headline line."""
+"""CPU checks of bench.py's guards (no GPU).
+
+* A ride-along leg that raises is reported inside the line, and the run then exits non-zero.
+* A leg that never finishes makes rank 0 print the line without it, and every rank exits non-zero.
+* The multi-rank dist_check (every rank's shard of the sharded key-switch / HomMult against its
+  single-device result) is exact on an honest gloo world-2 run, and a forced mismatch turns into a
+  non-zero exit after the line is printed.
+
+The driver's scaling runs therefore always get the headline line, and never read a hang, an error
+or a wrong answer as a success."""
 import json
 import os
+import socket
 import subprocess
 import sys
 
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from fhecore.dist import LimbShard, sharded_keyswitch  # noqa: E402
+
+
+def _fresh():
+    bench._EMIT.clear()
+    bench._EMIT["failed"] = []
 
 
 def test_guarded_leg_reports_exceptions():
-    sys.path.insert(0, ROOT)
-    import bench
+    _fresh()
 
     def boom():
         raise RuntimeError("no communicator")
 
     res = bench.guarded_leg(boom, {"metric": "m"}, 0, "keyswitch_leg", timeout_s=30)
     assert res == {"error": "RuntimeError: no communicator"}
+    assert bench._EMIT["failed"] == ["keyswitch_leg: RuntimeError"]
+    _fresh()
     assert bench.guarded_leg(lambda: {"value": 1}, {}, 0, "x", timeout_s=30) == {"value": 1}
+    assert bench.failure_reasons({"x": {"value": 1}}) == []
 
 
-def test_guarded_leg_timeout_emits_the_line():
-    code = f"""
+_LINE = """
 import argparse, os, sys, time
-sys.path.insert(0, {ROOT!r})
+sys.path.insert(0, {root!r})
 import bench
 bench._EMIT.update(json_fd=os.dup(1), args=argparse.Namespace(steps=3, warmup=1), world=1)
 out = {{"metric": "m", "value": 42.0, "unit": "HomMult/s", "ms_per_step": 1.0,
         "config": {{"workload": "w"}}}}
+"""
+
+
+def _run(body):
+    code = _LINE.format(root=ROOT) + body
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100)
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    return r, lines
+
+
+def test_guarded_leg_timeout_emits_the_line_and_fails():
+    r, lines = _run("""
 bench.guarded_leg(lambda: time.sleep(60), out, 0, "keyswitch_leg", timeout_s=1.0)
 print("not reached")
-"""
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=50)
-    assert r.returncode == 0
-    line = json.loads(r.stdout.strip().splitlines()[-1])
+""")
+    assert r.returncode == bench.EXIT_LEG_FAILED
+    assert len(lines) == 1
+    line = json.loads(lines[0])
     assert line["value"] == 42.0 and "did not finish" in line["keyswitch_leg"]["error"]
     assert "not reached" not in r.stdout
+
+
+def test_leg_error_prints_the_line_then_exits_nonzero():
+    r, lines = _run("""
+def boom():
+    raise RuntimeError("ncclAllGather failed")
+out["keyswitch_leg"] = bench.guarded_leg(boom, out, 0, "keyswitch_leg", timeout_s=30)
+sys.exit(bench.conclude(out, None, 0))
+""")
+    assert r.returncode == bench.EXIT_LEG_FAILED
+    line = json.loads(lines[0])
+    assert line["value"] == 42.0 and "ncclAllGather failed" in line["keyswitch_leg"]["error"]
+    assert "exiting 3" in r.stderr
+
+
+def test_dist_check_mismatch_prints_the_line_then_exits_nonzero():
+    r, lines = _run("""
+out["dist_check"] = {"result": "MISMATCH", "mismatched_words": 7, "checked": "x"}
+sys.exit(bench.conclude(out, None, 0))
+""")
+    assert r.returncode == bench.EXIT_LEG_FAILED
+    assert json.loads(lines[0])["dist_check"]["mismatched_words"] == 7
+
+
+def test_clean_run_exits_zero_and_emits_once():
+    r, lines = _run("""
+out["dist_check"] = {"result": "bit-exact", "checked": "x"}
+rc = bench.conclude(out, None, 0)
+assert not bench.emit_line(out, None)  # a second emit (e.g. a late watchdog) prints nothing
+sys.exit(rc)
+""")
+    assert r.returncode == 0, r.stderr
+    assert len(lines) == 1
+
+
+# ---- the dist_check itself at gloo world 2, against the CPU restatement of the engine ---------
+
+def _dist_worker(rank, world, port, corrupt, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from test_dist_cpu import K, L, CpuEngine, _data, _t
+
+        qs, ps, d2, eb, ea, a, b = _data(3)
+        eng = CpuEngine(qs, ps)
+        shard = LimbShard(L, world, rank)
+
+        def dist_fn(d, kb, ka):
+            k0, k1 = sharded_keyswitch(eng, d, kb, ka, shard)
+            if corrupt and rank == world - 1:
+                k0 = k0.clone()
+                k0.view(-1)[5] ^= 1
+            return k0, k1
+
+        bad = bench.check_keyswitch_shard(eng, shard, K, _t(d2), _t(eb), _t(ea), dist_fn)
+        bad += bench.check_hommult_shard(eng, shard, _t(a), _t(b))
+        t = torch.tensor([bad], dtype=torch.int64)
+        dist.all_reduce(t)
+        q.put((rank, int(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_dist_check_gloo_world2(corrupt):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, corrupt, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    got = dict(q.get() for _ in range(world))
+    # every rank sees the same summed count: all exit non-zero together on a mismatch
+    assert got == {0: (1 if corrupt else 0), 1: (1 if corrupt else 0)}
+
+
+def test_shard_mismatches_counts_only_own_limbs():
+    full = torch.arange(2 * 4 * 8, dtype=torch.int64).reshape(2, 4, 8)
+    sh = LimbShard(4, 2, 1)
+    got = full[:, 2:4].clone()
+    assert bench.shard_mismatches(got, full, sh) == 0
+    got[1, 0, 3] += 1
+    got[0, 1, 0] -= 1
+    assert bench.shard_mismatches(got, full, sh) == 2
+    assert bench.shard_mismatches(torch.empty(2, 0, 8), full, LimbShard(4, 8, 7)) == 0

@@ -45,6 +45,15 @@ class CpuEngine:
             return torch.empty(a.shape[:-3] + (3, 0, a.shape[-1]), dtype=torch.int64)
         return _t(coracle.hommult(_a(a), _a(b), self.qs[limb0:limb0 + nl]))
 
+    def keyswitch(self, d2, evk_b, evk_a):
+        """The single-device key-switch of the whole [batch, L, N] input (bench.dist_check's
+        reference side)."""
+        outs = [coracle.keyswitch(d, _a(evk_b), _a(evk_a), self.qs, self.ps, DNUM)
+                for d in _a(d2).reshape(-1, L, 1 << LOG_N)]
+        k0 = np.stack([o[0] for o in outs]).astype(np.uint64).reshape(d2.shape)
+        k1 = np.stack([o[1] for o in outs]).astype(np.uint64).reshape(d2.shape)
+        return _t(k0), _t(k1)
+
     def keyswitch_shard(self, c_all, d2_own, evk_b, evk_a, limb0, ranks=None):
         nl = d2_own.shape[-2]
         if nl == 0:
