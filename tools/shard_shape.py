@@ -34,6 +34,50 @@ def rate(fn, warmup, steps):
     return (time.perf_counter() - t0) / steps
 
 
+# xGMI on MI355X: 7 GPU-GPU links per GPU at 153.6 GB/s each, bidirectional (1075 GB/s aggregate),
+# so 76.8 GB/s per link and direction; a fully connected 8-GPU node gives every pair its own link.
+LINK_GBPS_DIR = 76.8
+
+
+def ks_partition_model(out, L, K, B, n):
+    """Per-rank time of one key-switch batch at N GPUs for the shipped partition (one all-gather of
+    the coefficient-form d2) and the P-sharded one (the same gather, plus an all-gather of the INTT'd
+    special-limb part of both accumulators, 2 K limbs per ciphertext, before ModDown), from the
+    measured rank-shape compute above and the bytes each rank receives.  Two link models: 'direct'
+    (every peer's block on its own link at the per-direction peak: the floor) and 'ring' (RCCL's
+    ring all-gather, bus bandwidth 0.7 of the 7-link aggregate).  Step time = max(compute, comm)
+    with the chunked overlap, and compute + comm without it."""
+    res = {"assumptions": {
+        "link_GBps_per_direction": LINK_GBPS_DIR,
+        "ring_bus_bandwidth_GBps": round(0.7 * 7 * LINK_GBPS_DIR, 1),
+        "batch": B, "bytes_per_limb_row": n * 8}}
+    row = n * 8
+    for G in (2, 4, 8):
+        c = -(-L // G)
+        d2_peer = B * c * row  # one peer's block of the d2 gather
+        kp = -(-K // G)        # special limbs a P-owning rank holds
+        owners = min(K, G)
+        p_peer = 2 * B * kp * row
+        variants = {
+            "replicated P (shipped)": (out[f"ks N={G}"]["ms_per_batch"],
+                                       [(G - 1, d2_peer)]),
+            "P-sharded": (out[f"ks N={G} P-sharded proxy"]["ms_per_batch"],
+                          [(G - 1, d2_peer), (owners - 1, p_peer)]),
+        }
+        for name, (comp, gathers) in variants.items():
+            recv = sum(k * b for k, b in gathers)
+            direct = sum(b for k, b in gathers if k) / (LINK_GBPS_DIR * 1e9) * 1e3
+            ring = recv / (0.7 * 7 * LINK_GBPS_DIR * 1e9) * 1e3  # received bytes / bus bandwidth
+            res[f"N={G} {name}"] = {
+                "compute_ms": comp, "recv_MB": round(recv / 1e6, 1),
+                "comm_ms_direct": round(direct, 4), "comm_ms_ring": round(ring, 4),
+                "step_ms_overlapped_direct": round(max(comp, direct), 4),
+                "step_ms_overlapped_ring": round(max(comp, ring), 4),
+                "step_ms_serial_ring": round(comp + ring, 4),
+                "keyswitch_per_s_overlapped_ring": round(B / max(comp, ring) * 1e3, 1)}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
@@ -65,7 +109,8 @@ def main():
         dn = rate(pair, args.warmup, args.steps)
         out[f"N={G}"] = {"limbs_per_gpu": sh.nlimbs, "ciphertexts_per_gpu": gb,
                          "hommult_ms_per_step": round(dt * 1e3, 4),
-                         "job_hommult_per_s_if_linear": round(gb * G / dt, 1),
+                         # each rank covers its limbs of all gb ciphertexts (bench.py hm_per_s)
+                         "job_hommult_per_s_if_linear": round(gb / dt, 1),
                          "per_gpu_poly_limb_hommults_per_s": round(gb * sh.nlimbs / dt, 1),
                          "ntt_pair_ms": round(dn * 1e3, 4),
                          "per_gpu_ntt_per_s": round(2 * npolys * sh.nlimbs / dn, 1)}
@@ -73,37 +118,46 @@ def main():
         torch.cuda.empty_cache()
     # key-switch leg, rank 0 of N: its limb shard of the leg's batch over a ranked gather region
     # filled with residues (timing only: the per-rank kernels of fhe_keyswitch_dist after its
-    # gather)
+    # gather).  "replicated P": the shipped partition (every rank extends into all K special
+    # limbs); "P-sharded proxy": the same shard on a context with ceil(K / N) special primes, the
+    # most loaded rank of a partition that deals the K special limbs out over the ranks (its
+    # ModDown conversion reads 1 P row instead of K: a slight under-estimate of that rank's work).
     Lk, K, dnum, B = 16, 4, 4, args.ks_batch
-    kctx = fc.Context(log_n, L=Lk, K=K, dnum=dnum)
     lib = load()
+    kctxs = {}
     for G in (1, 2, 4, 8):
-        sh = fdist.LimbShard(Lk, G, 0)
-        rows = sh.evk_rows(K)
-        allm = kctx.all_moduli
-        eb = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
-        ea = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
-        d2 = uniform_limbs(gen, kctx.moduli[sh.lo:sh.hi], (B,), n)
-        gat = torch.zeros(G * B * sh.width * n, dtype=torch.int64, device="cuda")
-        ks0 = kctx.empty(B, sh.nlimbs, n)
-        ks1 = kctx.empty(B, sh.nlimbs, n)
-        ws = kctx.workspace(lib.fhe_keyswitch_workspace(kctx.handle, sh.nlimbs, B))
+        for tag, kk in (("", K), (" P-sharded proxy", -(-K // G))):
+            kctx = kctxs.get(kk) or kctxs.setdefault(kk, fc.Context(log_n, L=Lk, K=kk, dnum=dnum))
+            sh = fdist.LimbShard(Lk, G, 0)
+            rows = sh.evk_rows(kk)
+            allm = kctx.all_moduli
+            eb = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
+            ea = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
+            d2 = uniform_limbs(gen, kctx.moduli[sh.lo:sh.hi], (B,), n)
+            gat = torch.zeros(G * B * sh.width * n, dtype=torch.int64, device="cuda")
+            ks0 = kctx.empty(B, sh.nlimbs, n)
+            ks1 = kctx.empty(B, sh.nlimbs, n)
+            ws = kctx.workspace(lib.fhe_keyswitch_workspace(kctx.handle, sh.nlimbs, B))
 
-        def ks():
-            rc = lib.fhe_keyswitch_shard_ranked(kctx.handle, ks0.data_ptr(), ks1.data_ptr(),
-                                                gat.data_ptr(), G, d2.data_ptr(), eb.data_ptr(),
-                                                ea.data_ptr(), sh.lo, sh.nlimbs, B,
-                                                ws.data_ptr(),
-                                                torch.cuda.current_stream().cuda_stream)
-            assert rc == 0, lib.fhe_last_error()
+            def ks():
+                kctx.intt(d2, limb0=sh.lo)  # the rank's INTT of its own limbs ahead of the gather
+                rc = lib.fhe_keyswitch_shard_ranked(kctx.handle, ks0.data_ptr(), ks1.data_ptr(),
+                                                    gat.data_ptr(), G, d2.data_ptr(),
+                                                    eb.data_ptr(), ea.data_ptr(), sh.lo,
+                                                    sh.nlimbs, B, ws.data_ptr(),
+                                                    torch.cuda.current_stream().cuda_stream)
+                assert rc == 0, lib.fhe_last_error()
 
-        dk = rate(ks, 20, 50)
-        out[f"ks N={G}"] = {"limbs_per_gpu": sh.nlimbs, "batch": B, "ms_per_batch": round(dk * 1e3, 4),
-                            "speedup_vs_N1_if_gather_hidden": None}
+            dk = rate(ks, 20, 50)
+            out[f"ks N={G}{tag}"] = {"limbs_per_gpu": sh.nlimbs, "special_limbs_per_gpu": kk,
+                                     "batch": B, "ms_per_batch": round(dk * 1e3, 4)}
+            del eb, ea, d2, gat, ks0, ks1, ws
     base = out["ks N=1"]["ms_per_batch"]
     for G in (1, 2, 4, 8):
-        out[f"ks N={G}"]["speedup_vs_N1_if_gather_hidden"] = round(
-            base / out[f"ks N={G}"]["ms_per_batch"], 3)
+        for tag in ("", " P-sharded proxy"):
+            out[f"ks N={G}{tag}"]["speedup_vs_N1_if_gather_hidden"] = round(
+                base / out[f"ks N={G}{tag}"]["ms_per_batch"], 3)
+    out["ks partition model"] = ks_partition_model(out, Lk, K, B, n)
     print(json.dumps(out, indent=1))
 
 
