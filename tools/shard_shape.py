@@ -43,13 +43,15 @@ def ks_partition_model(out, L, K, B, n):
     """Per-rank time of one key-switch batch at N GPUs for the shipped partition (one all-gather of
     the coefficient-form d2) and the P-sharded one (the same gather, plus an all-gather of the INTT'd
     special-limb part of both accumulators, 2 K limbs per ciphertext, before ModDown), from the
-    measured rank-shape compute above and the bytes each rank receives.  Two link models: 'direct'
-    (every peer's block on its own link at the per-direction peak: the floor) and 'ring' (RCCL's
-    ring all-gather, bus bandwidth 0.7 of the 7-link aggregate).  Step time = max(compute, comm)
-    with the chunked overlap, and compute + comm without it."""
+    measured rank-shape compute above and the bytes each rank receives.  N GPUs of one node reach
+    each other over N - 1 links (one per pair).  Two link models: 'direct' (every peer's block on
+    its own link at the per-direction peak: the floor) and 'ring' (RCCL's ring all-gather at a bus
+    bandwidth of 0.7 of the N - 1 links' aggregate).  Step time = max(compute, comm) with the
+    chunked overlap, and compute + comm without it."""
     res = {"assumptions": {
         "link_GBps_per_direction": LINK_GBPS_DIR,
-        "ring_bus_bandwidth_GBps": round(0.7 * 7 * LINK_GBPS_DIR, 1),
+        "links_between_N_gpus": "N - 1 per GPU (fully connected node, one link per pair)",
+        "ring_bus_bandwidth": "0.7 x (N - 1) x link_GBps_per_direction",
         "batch": B, "bytes_per_limb_row": n * 8}}
     row = n * 8
     for G in (2, 4, 8):
@@ -67,13 +69,14 @@ def ks_partition_model(out, L, K, B, n):
         for name, (comp, gathers) in variants.items():
             recv = sum(k * b for k, b in gathers)
             direct = sum(b for k, b in gathers if k) / (LINK_GBPS_DIR * 1e9) * 1e3
-            ring = recv / (0.7 * 7 * LINK_GBPS_DIR * 1e9) * 1e3  # received bytes / bus bandwidth
+            ring = recv / (0.7 * (G - 1) * LINK_GBPS_DIR * 1e9) * 1e3  # received / bus bandwidth
             res[f"N={G} {name}"] = {
                 "compute_ms": comp, "recv_MB": round(recv / 1e6, 1),
                 "comm_ms_direct": round(direct, 4), "comm_ms_ring": round(ring, 4),
                 "step_ms_overlapped_direct": round(max(comp, direct), 4),
                 "step_ms_overlapped_ring": round(max(comp, ring), 4),
                 "step_ms_serial_ring": round(comp + ring, 4),
+                "keyswitch_per_s_overlapped_direct": round(B / max(comp, direct) * 1e3, 1),
                 "keyswitch_per_s_overlapped_ring": round(B / max(comp, ring) * 1e3, 1)}
     return res
 
@@ -162,4 +165,12 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == "--remodel":
+        # recompute the model from a saved run's measured rank shapes (no GPU)
+        with open(sys.argv[2]) as f:
+            saved = json.load(f)
+        saved["ks partition model"] = ks_partition_model(saved, 16, 4, saved["ks N=1"]["batch"],
+                                                         1 << 16)
+        print(json.dumps(saved, indent=1))
+    else:
+        main()
