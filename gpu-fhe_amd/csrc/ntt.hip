@@ -41,6 +41,10 @@ constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per work
 // tiles, measured -4 % on the N = 2^17 ntt-batch column pass and +9 % on the HomMult column
 // inverse; 256 kept everywhere.)
 constexpr int kColThreads = kThreads;
+#ifndef FHE_COL_HALF
+#define FHE_COL_HALF 1
+#endif
+
 // Occupancy the register allocator / scheduler may assume (waves per SIMD): LDS caps these kernels
 // at 4 workgroups (16 waves) per CU, so a lower target costs no waves and lets the scheduler spend
 // VGPRs on interleaving independent butterflies; anything above 128 VGPRs would cost waves.
@@ -643,6 +647,78 @@ struct LViewC {
   }
 };
 
+// Column-pass round exchange through half the tile's LDS (pass_run HALF).  The top position bit
+// T = 2^(LOGR-1) splits the tile into two halves that each round layout keeps together: in one
+// layout T is an element bit (a thread holds both halves, 8 elements each), in the other a thread
+// bit (a thread holds one half, all 16 elements; t = threadIdx.x / SUBS, so that bit is uniform
+// per wavefront).  Half h goes through the one buffer (positions p & (T - 1)) in phase h:
+//   writer holds both halves (forward): every thread writes its half-h elements; barrier; the
+//     threads of half h read theirs.  The half-0 readers still owe their half-1 elements to phase
+//     1, so they read into y and keep x until then.
+//   reader holds both halves (inverse): the threads of half h write all of theirs; barrier; every
+//     thread reads its half-h elements.  The half-1 writers read phase 0's elements into y,
+//     keeping x for their phase-1 write.
+// 16 KB per tile instead of 32 KB at LOGR = 8, 16 columns: LDS no longer caps the column
+// passes at 5 workgroups per CU.  The caller has no LDS access outstanding on the buffer.
+template <int LOGR, class LayW, class LayR, class LV>
+__device__ __forceinline__ void half_exchange(u64 (&x)[kE], const LV& lv, u32 t) {
+  constexpr u32 T = 1u << (LOGR - 1);
+  constexpr bool w_both = (LayW::jmask & T) != 0;
+  constexpr bool r_both = (LayR::jmask & T) != 0;
+  static_assert(w_both != r_both, "the top bit must be an element bit in exactly one layout");
+  const u32 tpw = LayW::tpos(t), tpr = LayR::tpos(t);
+  u64 y[kE];
+  if constexpr (w_both) {
+    const bool hr = (tpr & T) != 0;  // this thread's half as a reader (wave-uniform)
+    static_for<0, 2>([&](auto hc) {
+      constexpr u32 h = decltype(hc)::value;
+      if constexpr (h == 1) __syncthreads();  // phase 0's reads are done
+#pragma unroll
+      for (int j = 0; j < kE; ++j) {
+        if (((LayW::jpos(j) & T) != 0) != (h == 1)) continue;
+        // the half-0 readers hold their half-1 elements in y (phase 0 replaced x)
+        lv.s[lv.idx((tpw | LayW::jpos(j)) & (T - 1))] = (h == 1 && !hr) ? y[j] : x[j];
+      }
+      __syncthreads();
+      if (hr == (h == 1)) {
+#pragma unroll
+        for (int j = 0; j < kE; ++j) {
+          if (h == 0) y[j] = x[j];
+          x[j] = lv.s[lv.idx((tpr | LayR::jpos(j)) & (T - 1))];
+        }
+      }
+    });
+  } else {
+    const bool hw = (tpw & T) != 0;  // this thread's half as a writer (wave-uniform)
+    static_for<0, 2>([&](auto hc) {
+      constexpr u32 h = decltype(hc)::value;
+      if constexpr (h == 1) __syncthreads();
+      if (hw == (h == 1)) {
+#pragma unroll
+        for (int j = 0; j < kE; ++j) lv.s[lv.idx((tpw | LayW::jpos(j)) & (T - 1))] = x[j];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kE; ++j) {
+        if (((LayR::jpos(j) & T) != 0) != (h == 1)) continue;
+        const u64 v = lv.s[lv.idx((tpr | LayR::jpos(j)) & (T - 1))];
+        if (h == 0 && hw) {
+          y[j] = v;  // x still owes phase 1 its write
+        } else {
+          x[j] = v;
+        }
+      }
+      if constexpr (h == 1) {
+        if (hw) {
+#pragma unroll
+          for (int j = 0; j < kE; ++j)
+            if ((LayR::jpos(j) & T) == 0) x[j] = y[j];
+        }
+      }
+    });
+  }
+}
+
 // Round-0 global load of one sub-transform into registers.
 template <int LOGR, bool FWD, class GIn>
 __device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
@@ -658,8 +734,9 @@ __device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
 // XOUT: the last round goes out through the LDS in linear order (GView::store_lin) instead of
 // straight from registers, whose last-round positions are E consecutive words per thread, so a
 // direct store instruction writes 16 of every 16 E bytes across 16 E * 64 bytes.
+// HALF: the column passes' one exchange (two rounds) through half the tile's LDS (half_exchange).
 template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, int H, int R0, bool XOUT = false,
-          bool CHAIN = GATHER, class GOut, class LV>
+          bool CHAIN = GATHER, bool HALF = false, class GOut, class LV>
 __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const LV& lv, u32 t,
                                          const ulonglong2* __restrict__ tw, u32 base, u64 q,
                                          ulonglong2 nf0, ulonglong2 nf1) {
@@ -672,7 +749,8 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     constexpr int RIN = fwd_range(R0, Rd::lo_fwd(0) + Rd::kb(0) - (LO + KB), H);  // stages before
     using Lay = Layout<LOGR, KB, LO>;
     const u32 tp = Lay::tpos(t);
-    if constexpr (k > 0) {
+    static_assert(!HALF || (Rd::NR == 2 && SYNC == kBlockSync), "half exchange: column, 2 rounds");
+    if constexpr (k > 0 && !HALF) {  // (HALF: half_exchange already loaded this round's layout)
       lds_sync<SYNC>();
       lv.template load<Lay>(x, tp);
     }
@@ -698,6 +776,10 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
       } else {
         gout.template store<Lay>(x, tp);
       }
+    } else if constexpr (HALF) {
+      constexpr int KN = FWD ? Rd::kb(k + 1) : Rd::kb_inv(k + 1);
+      constexpr int LN = FWD ? Rd::lo_fwd(k + 1) : Rd::lo_inv(k + 1);
+      half_exchange<LOGR, Lay, Layout<LOGR, KN, LN>>(x, lv, t);
     } else {
       // the (free) wave-local fence before round 0's store keeps the row passes' LDS stores
       // together after the butterflies, which measured faster than letting them interleave
@@ -717,6 +799,12 @@ struct Geo {
   static constexpr int THR_C = SUBS_C * TPS_C;
   static constexpr int LDS_C = R1 * SUBS_C;  // LViewC: no padding
   static_assert(SUBS_C == 16 || SUBS_C >= 32, "column LDS layout assumes 16 or >= 32 columns");
+  // the forward column passes exchange through half the tile (half_exchange) where their two
+  // rounds are 4 + 4 stages over 16 columns (N = 2^16, 2^17): 16 KB per workgroup.  (The inverse
+  // column passes measured 2-3 % slower that way -- their writers hold one half, so half the waves
+  // keep 8 values across a phase -- and keep the full tile: DESIGN.md §8.)
+  static constexpr bool HALF_C = FHE_COL_HALF && N1 == 8 && SUBS_C == 16;
+  static constexpr int LDS_CF = HALF_C ? LDS_C / 2 : LDS_C;  // forward column passes
   static constexpr int TILES_C = R2 / SUBS_C;
   // row pass: SUBS_R rows per workgroup, lanes run along a row
   static constexpr int TPS_R = R2 >> kElog;
@@ -738,8 +826,8 @@ struct Geo {
 // follows must assume the same R0: fwd_range is not monotonic in it (an earlier reduction can leave
 // a smaller bound), so the key-switch / rescale row kernels, which assume 2 (k_modup_col's
 // outputs), get column passes scheduled from 2 as well (col_fwd_pass, k_rescale_col).
-// One column tile (poly p, limb l, tile) of a column pass (the body of k_ntt_col; lds: G::LDS_C
-// words).
+// One column tile (poly p, limb l, tile) of a column pass (the body of k_ntt_col; lds: G::LDS_CF
+// words forward, G::LDS_C inverse).
 template <int LOGN, bool FWD, int H, bool NTL, bool NTS, int FI, int R0>
 __device__ __forceinline__ void col_tile(u64* lds, const u64* __restrict__ src,
                                          const u64* __restrict__ src2, u64* __restrict__ dst,
@@ -761,7 +849,8 @@ __device__ __forceinline__ void col_tile(u64* lds, const u64* __restrict__ src,
     nf0 = nfold[4 * limb];
     nf1 = nfold[4 * limb + 1];
   }
-  pass_run<G::N1, FWD, FWD ? kNotFinal : FI, kBlockSync, false, H, R0>(
+  pass_run<G::N1, FWD, FWD ? kNotFinal : FI, kBlockSync, false, H, R0, false, false,
+           FWD && G::HALF_C>(
       x, GView<G::R2, false, NTS>{dst + pm.dst(p) + loc, sub}, lv, t, tw_all + (u64)limb * N, 1u,
       mods[limb].q, nf0, nf1);
 }
@@ -773,7 +862,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 
     u32 limb0, PolyMap pm, u32 items, const ulonglong2* __restrict__ tw_all,
     const ulonglong2* __restrict__ nfold, const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
-  __shared__ u64 lds[G::LDS_C];
+  __shared__ u64 lds[FWD ? G::LDS_CF : G::LDS_C];
   const u32 it = blockIdx.x;
   if (it >= items) return;
   // XCD-grouped placement: workgroups are dealt to the 8 XCDs round-robin, so XCD x takes the
@@ -1069,7 +1158,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   using Rd = Rounds<G::N1>;
   using Lay0 = Layout<G::N1, Rd::kb(0), Rd::lo_fwd(0)>;
   constexpr u64 N = 1ull << LOGN;
-  __shared__ u64 lds[G::LDS_C];
+  __shared__ u64 lds[G::LDS_CF];
   const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
   const LViewC<G::SUBS_C> lv{lds + sub};
   u32 di = 0;
@@ -1137,7 +1226,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   // mad-chain remainders (CHAIN) although this is a column pass: unlike the latency-bound column
   // passes of the NTTs, this one is VALU-bound (the conversion products): ModUp -1.1 %, ModDown
   // conversion pass -1 % same-box (profiles/r03_modup_chain_ab.txt)
-  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2, false, true>(
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2, false, true, G::HALF_C>(
       x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
       tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
 }
@@ -1557,7 +1646,7 @@ k_rescale_col(const u64* __restrict__ last, u64* __restrict__ dst, u32 nq, u32 i
               const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
   constexpr u64 N = 1ull << LOGN;
-  __shared__ u64 lds[G::LDS_C];
+  __shared__ u64 lds[G::LDS_CF];
   const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
   const LViewC<G::SUBS_C> lv{lds + sub};
   const u32 it = blockIdx.x;
@@ -1587,7 +1676,7 @@ k_rescale_col(const u64* __restrict__ last, u64* __restrict__ dst, u32 nq, u32 i
 #pragma unroll
   for (int j = 0; j < kE; ++j) x[j] = csub(reduce_word(csub(x[j] + h, ml.q), mi) + mh, mi.q);
   // scheduled from 2 (inputs are below q): the range k_moddown_row assumes
-  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2>(
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2, false, false, G::HALF_C>(
       x, GView<G::R2>{dst + (u64)pl * N + col, sub}, lv, t, tw_all + (u64)l * N, 1u, mi.q,
       {0, 0}, {0, 0});
 }

@@ -502,3 +502,116 @@ def test_lazy_gs_round(q):
             if r > 3:
                 x[j] = top_bits(x[j], q)
             assert x[j] < q3 and x[j] % q == ref[j]
+
+
+# ---- ntt.hip half_exchange: the column passes' round exchange through half the tile's LDS ------
+# Python restatement of ntt.hip's Rounds / Layout / LViewC<16> index maps and of half_exchange's two
+# phases, run for every thread of one column (16 threads x 16 elements at log R1 = 8): each thread
+# must end holding exactly the positions of the next round's layout, and no phase may write one LDS
+# word twice.
+
+_KELOG, _KE = 4, 16
+
+
+def _rounds(logr):
+    nr = (logr + _KELOG - 1) // _KELOG
+    kb = [logr // nr + (1 if k < logr % nr else 0) for k in range(nr)]
+    lo = []
+    hi = logr
+    for k in range(nr):
+        hi -= kb[k]
+        lo.append(hi)
+    return nr, kb, lo
+
+
+class _Layout:
+    def __init__(self, logr, kb, lo):
+        self.logr, self.kb, self.lo = logr, kb, lo
+        free = [i for i in range(logr) if not lo <= i < lo + kb]
+        self.ex = free
+        self.jmask = self.jpos(_KE - 1)
+
+    def jpos(self, j):
+        p = 0
+        for b in range(self.kb):
+            if (j >> b) & 1:
+                p |= 1 << (self.lo + b)
+        for b in range(_KELOG - self.kb):
+            if (j >> (self.kb + b)) & 1:
+                p |= 1 << self.ex[b]
+        return p
+
+    def tpos(self, t):
+        p, k = 0, 0
+        for i in range(self.logr):
+            if (self.jmask >> i) & 1:
+                continue
+            p |= ((t >> k) & 1) << i
+            k += 1
+        return p
+
+
+def _lviewc16(p):
+    return (p >> 1) * 32 + (((p ^ (p >> 4)) & 1) << 4)
+
+
+@pytest.mark.parametrize("fwd", [True, False])
+def test_half_exchange_layouts(fwd):
+    logr = 8
+    nr, kb, lo = _rounds(logr)
+    assert nr == 2
+    ks = (0, 1) if fwd else (1, 0)  # the inverse runs the forward's rounds mirrored
+    W, R = _Layout(logr, kb[ks[0]], lo[ks[0]]), _Layout(logr, kb[ks[1]], lo[ks[1]])
+    T = 1 << (logr - 1)
+    tps = (1 << logr) // _KE
+    w_both, r_both = bool(W.jmask & T), bool(R.jmask & T)
+    assert w_both != r_both and w_both == fwd
+    # the half bit of a one-half layout is a thread bit: t = threadIdx.x / 16 within a 256-thread
+    # workgroup, so it must be constant over each wavefront's 4 values of t
+    one = R if w_both else W
+    for w in range(4):
+        assert len({bool(one.tpos(t) & T) for t in range(4 * w, 4 * w + 4)}) == 1
+    x = {t: [W.tpos(t) | W.jpos(j) for j in range(_KE)] for t in range(tps)}
+    y = {t: [None] * _KE for t in range(tps)}
+    for h in (0, 1):
+        lds, written = {}, set()
+
+        def put(i, v):
+            assert i not in written and 0 <= i < 2048
+            written.add(i)
+            lds[i] = v
+
+        if w_both:
+            for t in range(tps):
+                hr = bool(R.tpos(t) & T)
+                for j in range(_KE):
+                    if bool(W.jpos(j) & T) == (h == 1):
+                        put(_lviewc16((W.tpos(t) | W.jpos(j)) & (T - 1)),
+                            y[t][j] if (h == 1 and not hr) else x[t][j])
+            for t in range(tps):
+                if bool(R.tpos(t) & T) == (h == 1):
+                    for j in range(_KE):
+                        if h == 0:
+                            y[t][j] = x[t][j]
+                        x[t][j] = lds[_lviewc16((R.tpos(t) | R.jpos(j)) & (T - 1))]
+        else:
+            for t in range(tps):
+                if bool(W.tpos(t) & T) == (h == 1):
+                    for j in range(_KE):
+                        put(_lviewc16((W.tpos(t) | W.jpos(j)) & (T - 1)), x[t][j])
+            for t in range(tps):
+                hw = bool(W.tpos(t) & T)
+                for j in range(_KE):
+                    if bool(R.jpos(j) & T) == (h == 1):
+                        v = lds[_lviewc16((R.tpos(t) | R.jpos(j)) & (T - 1))]
+                        if h == 0 and hw:
+                            y[t][j] = v
+                        else:
+                            x[t][j] = v
+                if h == 1 and hw:
+                    for j in range(_KE):
+                        if not R.jpos(j) & T:
+                            x[t][j] = y[t][j]
+        assert len(written) == 128  # one column's half: 128 words of the 16 KB buffer
+    for t in range(tps):
+        assert x[t] == [R.tpos(t) | R.jpos(j) for j in range(_KE)]
