@@ -670,13 +670,19 @@ def run_ntt_batch(args, world, rank):
 
 
 def valu_profile():
-    """profiles/r03_keyswitch_pmc.json: per-kernel SQ_INSTS_VALU per launch of the key-switch at
-    the bench shape (rocprofv3 --pmc pass, tools/valu_roofline.py), or None."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "r03_keyswitch_pmc.json")) as f:
-            return json.load(f)
-    except (OSError, ValueError):
-        return None
+    """The newest profiles/rNN_keyswitch_pmc.json: per-kernel SQ_INSTS_VALU per launch of the
+    key-switch at the bench shape (rocprofv3 --pmc pass, tools/valu_roofline.py), with its file
+    name, or (None, None)."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_keyswitch_pmc.json")))
+    for path in reversed(paths):
+        try:
+            with open(path) as f:
+                return json.load(f), os.path.relpath(path, ROOT)
+        except (OSError, ValueError):
+            continue
+    return None, None
 
 
 class KeyswitchLeg:
@@ -757,7 +763,7 @@ class KeyswitchLeg:
         # conversion products, inner products, reductions, addressing): SQ_INSTS_VALU per launch
         # of each key-switch kernel at this shape (committed rocprofv3 --pmc pass) over this run's
         # time, against the issue rate of the butterfly ceiling kernel in that profiled process
-        prof = valu_profile()
+        prof, prof_path = valu_profile()
         if prof and world == 1 and B == prof.get("shape", {}).get("batch"):
             per_step = sum(v["valu_instr_per_launch"] * v["launches_per_step"]
                            for k, v in prof["kernels"].items() if k.startswith("k_") and
@@ -767,7 +773,7 @@ class KeyswitchLeg:
                 "bound": "valu", "achieved": round(ach, 1), "peak": prof["ceiling_valu_g_per_s"],
                 "unit": "G VALU wave-instructions/s", "frac": round(ach / prof["ceiling_valu_g_per_s"], 4),
                 "valu_instr_per_step": per_step,
-                "valu_source": "committed, not measured in this run: profiles/r03_keyswitch_pmc.json "
+                "valu_source": f"committed, not measured in this run: {prof_path} "
                                "(SQ_INSTS_VALU of every key-switch kernel, same shape); time from this run",
                 "per_kernel_frac_of_peak": {k: v.get("frac_of_bfly_peak_issue")
                                             for k, v in prof["kernels"].items()

@@ -6,7 +6,7 @@ log=$1; to=$2; shift 2
 for i in $(seq 1 40); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@" > "$log" 2>&1
   rc=$?
-  if grep -q "status=transient\|no free box\|backing off\|stopped responding while being prepared" "$log" && ! grep -q "status=ok\|status=fail" "$log"; then
+  if grep -q "status=transient\|no free box\|backing off\|stopped responding while being prepared\|taken away by the GPU service" "$log" && ! grep -q "status=ok\|status=fail" "$log"; then
     sleep 90; continue
   fi
   exit $rc
