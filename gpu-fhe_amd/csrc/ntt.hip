@@ -41,9 +41,6 @@ constexpr int kThreads = 4096 / kE;  // 16 sub-transforms of 256 points per work
 // tiles, measured -4 % on the N = 2^17 ntt-batch column pass and +9 % on the HomMult column
 // inverse; 256 kept everywhere.)
 constexpr int kColThreads = kThreads;
-#ifndef FHE_COL_HALF
-#define FHE_COL_HALF 1
-#endif
 
 // Occupancy the register allocator / scheduler may assume (waves per SIMD): LDS caps these kernels
 // at 4 workgroups (16 waves) per CU, so a lower target costs no waves and lets the scheduler spend
@@ -596,8 +593,13 @@ struct GView {
       x[2 * jj + 1] = w.y;
     }
   }
+  struct NoPre {};
   template <u32 TPS>
-  __device__ __forceinline__ void store_lin(const u64 (&x)[kE], u32 t) const {
+  __device__ __forceinline__ NoPre pre_lin(u32) const {
+    return {};
+  }
+  template <u32 TPS>
+  __device__ __forceinline__ void store_lin(const u64 (&x)[kE], u32 t, NoPre = {}) const {
     static_assert(STRIDE == 1, "rows only");
     const gptr_u128 v = (gptr_u128)(base + lane) + t;
 #pragma unroll
@@ -647,76 +649,54 @@ struct LViewC {
   }
 };
 
-// Column-pass round exchange through half the tile's LDS (pass_run HALF).  The top position bit
-// T = 2^(LOGR-1) splits the tile into two halves that each round layout keeps together: in one
-// layout T is an element bit (a thread holds both halves, 8 elements each), in the other a thread
-// bit (a thread holds one half, all 16 elements; t = threadIdx.x / SUBS, so that bit is uniform
-// per wavefront).  Half h goes through the one buffer (positions p & (T - 1)) in phase h:
-//   writer holds both halves (forward): every thread writes its half-h elements; barrier; the
-//     threads of half h read theirs.  The half-0 readers still owe their half-1 elements to phase
-//     1, so they read into y and keep x until then.
-//   reader holds both halves (inverse): the threads of half h write all of theirs; barrier; every
-//     thread reads its half-h elements.  The half-1 writers read phase 0's elements into y,
-//     keeping x for their phase-1 write.
-// 16 KB per tile instead of 32 KB at LOGR = 8, 16 columns: LDS no longer caps the column
-// passes at 5 workgroups per CU.  The caller has no LDS access outstanding on the buffer.
+// Column-pass round exchange through half the tile's LDS (pass_run HALF).  A split bit SB of the
+// position is an element bit in the writing round's layout and a thread bit -- uniform per
+// wavefront (t = threadIdx.x / SUBS) -- in the reading round's: the forward's top bit, the
+// inverse's bit 3 (the top bit of its first round).  The tile's two halves (positions with bit
+// SB = h) then go through one buffer, positions compressed to LOGR - 1 bits, in phase h: every
+// thread writes its 8 half-h elements; barrier; the threads of half h read all 16 of theirs.
+// The half-0 readers still owe their half-1 elements to phase 1, so they read into x after
+// copying those 8 values to y.  16 KB per tile instead of 32 KB at LOGR = 8, 16 columns: LDS no
+// longer caps the column passes at 5 workgroups per CU.  Every layout pair is conflict-free in
+// the LDS banks (same cycles as the full-tile exchange) and is model-checked in
+// tests/test_modarith_model.py::test_half_exchange_layouts.  The caller has no LDS access
+// outstanding on the buffer.
+template <u32 WJ, u32 RJ>
+constexpr int half_split_bit() {
+  for (int b = 31; b >= 0; --b)
+    if (((WJ & ~RJ) >> b) & 1u) return b;
+  return -1;
+}
+template <int SB>
+__device__ __forceinline__ u32 half_pos(u32 p) {
+  return (p & ((1u << SB) - 1)) | ((p >> (SB + 1)) << SB);
+}
 template <int LOGR, class LayW, class LayR, class LV>
 __device__ __forceinline__ void half_exchange(u64 (&x)[kE], const LV& lv, u32 t) {
-  constexpr u32 T = 1u << (LOGR - 1);
-  constexpr bool w_both = (LayW::jmask & T) != 0;
-  constexpr bool r_both = (LayR::jmask & T) != 0;
-  static_assert(w_both != r_both, "the top bit must be an element bit in exactly one layout");
+  constexpr int SB = half_split_bit<LayW::jmask, LayR::jmask>();
+  static_assert(SB >= 0 && SB < LOGR, "no element bit of the writer is a thread bit of the reader");
+  constexpr u32 S = 1u << SB;
   const u32 tpw = LayW::tpos(t), tpr = LayR::tpos(t);
+  const bool hr = (tpr & S) != 0;  // this thread's half as a reader (wave-uniform)
   u64 y[kE];
-  if constexpr (w_both) {
-    const bool hr = (tpr & T) != 0;  // this thread's half as a reader (wave-uniform)
-    static_for<0, 2>([&](auto hc) {
-      constexpr u32 h = decltype(hc)::value;
-      if constexpr (h == 1) __syncthreads();  // phase 0's reads are done
+  static_for<0, 2>([&](auto hc) {
+    constexpr u32 h = decltype(hc)::value;
+    if constexpr (h == 1) __syncthreads();  // phase 0's reads are done
+#pragma unroll
+    for (int j = 0; j < kE; ++j) {
+      if (((LayW::jpos(j) & S) != 0) != (h == 1)) continue;
+      // the half-0 readers hold their half-1 elements in y (phase 0 replaced x)
+      lv.s[lv.idx(half_pos<SB>(tpw | LayW::jpos(j)))] = (h == 1 && !hr) ? y[j] : x[j];
+    }
+    __syncthreads();
+    if (hr == (h == 1)) {
 #pragma unroll
       for (int j = 0; j < kE; ++j) {
-        if (((LayW::jpos(j) & T) != 0) != (h == 1)) continue;
-        // the half-0 readers hold their half-1 elements in y (phase 0 replaced x)
-        lv.s[lv.idx((tpw | LayW::jpos(j)) & (T - 1))] = (h == 1 && !hr) ? y[j] : x[j];
+        if (h == 0) y[j] = x[j];
+        x[j] = lv.s[lv.idx(half_pos<SB>(tpr | LayR::jpos(j)))];
       }
-      __syncthreads();
-      if (hr == (h == 1)) {
-#pragma unroll
-        for (int j = 0; j < kE; ++j) {
-          if (h == 0) y[j] = x[j];
-          x[j] = lv.s[lv.idx((tpr | LayR::jpos(j)) & (T - 1))];
-        }
-      }
-    });
-  } else {
-    const bool hw = (tpw & T) != 0;  // this thread's half as a writer (wave-uniform)
-    static_for<0, 2>([&](auto hc) {
-      constexpr u32 h = decltype(hc)::value;
-      if constexpr (h == 1) __syncthreads();
-      if (hw == (h == 1)) {
-#pragma unroll
-        for (int j = 0; j < kE; ++j) lv.s[lv.idx((tpw | LayW::jpos(j)) & (T - 1))] = x[j];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < kE; ++j) {
-        if (((LayR::jpos(j) & T) != 0) != (h == 1)) continue;
-        const u64 v = lv.s[lv.idx((tpr | LayR::jpos(j)) & (T - 1))];
-        if (h == 0 && hw) {
-          y[j] = v;  // x still owes phase 1 its write
-        } else {
-          x[j] = v;
-        }
-      }
-      if constexpr (h == 1) {
-        if (hw) {
-#pragma unroll
-          for (int j = 0; j < kE; ++j)
-            if ((LayR::jpos(j) & T) == 0) x[j] = y[j];
-        }
-      }
-    });
-  }
+    }
+  });
 }
 
 // Round-0 global load of one sub-transform into registers.
@@ -763,6 +743,9 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     if constexpr (k == Rd::NR - 1) {
       if constexpr (XOUT) {
         constexpr u32 TPS = (1u << LOGR) / kE;
+        // an output view that reads operands at the store positions (FinishView's acc rows)
+        // issues those loads here, so they are in flight during the LDS transposition
+        const auto pre = gout.template pre_lin<TPS>(t);
         lds_sync<SYNC>();
         lv.template store<Lay>(x, tp);
         lds_sync<SYNC>();
@@ -772,7 +755,7 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
           x[2 * jj] = lv.s[lv.idx(p)];
           x[2 * jj + 1] = lv.s[lv.idx(p + 1)];
         }
-        gout.template store_lin<TPS>(x, t);
+        gout.template store_lin<TPS>(x, t, pre);
       } else {
         gout.template store<Lay>(x, tp);
       }
@@ -799,12 +782,10 @@ struct Geo {
   static constexpr int THR_C = SUBS_C * TPS_C;
   static constexpr int LDS_C = R1 * SUBS_C;  // LViewC: no padding
   static_assert(SUBS_C == 16 || SUBS_C >= 32, "column LDS layout assumes 16 or >= 32 columns");
-  // the forward column passes exchange through half the tile (half_exchange) where their two
-  // rounds are 4 + 4 stages over 16 columns (N = 2^16, 2^17): 16 KB per workgroup.  (The inverse
-  // column passes measured 2-3 % slower that way -- their writers hold one half, so half the waves
-  // keep 8 values across a phase -- and keep the full tile: DESIGN.md §8.)
-  static constexpr bool HALF_C = FHE_COL_HALF && N1 == 8 && SUBS_C == 16;
-  static constexpr int LDS_CF = HALF_C ? LDS_C / 2 : LDS_C;  // forward column passes
+  // the column passes exchange through half the tile (half_exchange) where their two rounds are
+  // 4 + 4 stages over 16 columns (N = 2^16, 2^17): 16 KB per workgroup
+  static constexpr bool HALF_C = N1 == 8 && SUBS_C == 16;
+  static constexpr int LDS_CF = HALF_C ? LDS_C / 2 : LDS_C;
   static constexpr int TILES_C = R2 / SUBS_C;
   // row pass: SUBS_R rows per workgroup, lanes run along a row
   static constexpr int TPS_R = R2 >> kElog;
@@ -827,7 +808,7 @@ struct Geo {
 // a smaller bound), so the key-switch / rescale row kernels, which assume 2 (k_modup_col's
 // outputs), get column passes scheduled from 2 as well (col_fwd_pass, k_rescale_col).
 // One column tile (poly p, limb l, tile) of a column pass (the body of k_ntt_col; lds: G::LDS_CF
-// words forward, G::LDS_C inverse).
+// words).
 template <int LOGN, bool FWD, int H, bool NTL, bool NTS, int FI, int R0>
 __device__ __forceinline__ void col_tile(u64* lds, const u64* __restrict__ src,
                                          const u64* __restrict__ src2, u64* __restrict__ dst,
@@ -849,8 +830,7 @@ __device__ __forceinline__ void col_tile(u64* lds, const u64* __restrict__ src,
     nf0 = nfold[4 * limb];
     nf1 = nfold[4 * limb + 1];
   }
-  pass_run<G::N1, FWD, FWD ? kNotFinal : FI, kBlockSync, false, H, R0, false, false,
-           FWD && G::HALF_C>(
+  pass_run<G::N1, FWD, FWD ? kNotFinal : FI, kBlockSync, false, H, R0, false, false, G::HALF_C>(
       x, GView<G::R2, false, NTS>{dst + pm.dst(p) + loc, sub}, lv, t, tw_all + (u64)limb * N, 1u,
       mods[limb].q, nf0, nf1);
 }
@@ -862,7 +842,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 
     u32 limb0, PolyMap pm, u32 items, const ulonglong2* __restrict__ tw_all,
     const ulonglong2* __restrict__ nfold, const ModParams* __restrict__ mods) {
   using G = Geo<LOGN>;
-  __shared__ u64 lds[FWD ? G::LDS_CF : G::LDS_C];
+  __shared__ u64 lds[G::LDS_CF];
   const u32 it = blockIdx.x;
   if (it >= items) return;
   // XCD-grouped placement: workgroups are dealt to the 8 XCDs round-robin, so XCD x takes the
@@ -1277,13 +1257,23 @@ struct FinishView {
       o[j] = plus(u64x2_t{r0, r1}, off + 2 * j);
     }
   }
+  struct Pre {
+    u64x2_t a[kE / 2];
+  };
   template <u32 TPS>
-  __device__ __forceinline__ void store_lin(const u64 (&x)[kE], u32 t) const {
+  __device__ __forceinline__ Pre pre_lin(u32 t) const {
+    Pre pre;
     const gptr_u128 a = (gptr_u128)(acc + lane) + t;
+#pragma unroll
+    for (int jj = 0; jj < kE / 2; ++jj) pre.a[jj] = a[jj * TPS];
+    return pre;
+  }
+  template <u32 TPS>
+  __device__ __forceinline__ void store_lin(const u64 (&x)[kE], u32 t, const Pre& pre) const {
     const gptr_u128 o = (gptr_u128)(out + lane) + t;
 #pragma unroll
     for (int jj = 0; jj < kE / 2; ++jj) {
-      const u64x2_t av = a[jj * TPS];
+      const u64x2_t av = pre.a[jj];
       const u64 r0 = csub(shoup_lazy(av.x + q - x[2 * jj], pinv.x, pinv.y, q), q);
       const u64 r1 = csub(shoup_lazy(av.y + q - x[2 * jj + 1], pinv.x, pinv.y, q), q);
       o[jj * TPS] = plus(u64x2_t{r0, r1}, lane + 2 * (t + jj * TPS));
@@ -1441,16 +1431,27 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
       own_slot.template store<LayT>(v, tpT);
     }
   }
-  __syncthreads();
   // combine: the workgroup's ROWS x R2 positions are re-dealt so that each thread takes CW
   // consecutive positions of one row and a wavefront covers contiguous words (coalesced 16-byte
-  // key loads and output stores)
+  // key loads and output stores).  The key words do not depend on the other digits' rows, so
+  // every thread issues its loads before the barrier: they are in flight while the slower
+  // digits finish their NTTs (and the own digit's wave, which only loaded d2, waits for them).
   constexpr int CW = (H::ROWS * G::R2) / H::THR;
   static_assert(CW == 4 || CW == 2 || CW == 8, "combine width");
   const u32 cpos0 = threadIdx.x * CW;
   const u32 crow = cpos0 / G::R2, cpos = cpos0 % G::R2;
   const u64 okey = (u64)r * N + (u64)(tile * H::ROWS + crow) * G::R2 + cpos;
   const u64* lrow = lds + crow * H::ROWW;
+  u64x2_t kbv[CW / 2][DNUM], kav[CW / 2][DNUM];
+#pragma unroll
+  for (int e = 0; e < CW; e += 2) {
+#pragma unroll
+    for (int d = 0; d < DNUM; ++d) {
+      kbv[e / 2][d] = *(const __attribute__((address_space(1))) u64x2_t*)(evk_b + (u64)d * rn + okey + e);
+      kav[e / 2][d] = *(const __attribute__((address_space(1))) u64x2_t*)(evk_a + (u64)d * rn + okey + e);
+    }
+  }
+  __syncthreads();
   u64 o0[CW], o1[CW];
   u64 qi = 0 - m.qinv;  // q^-1 mod 2^64 (MONT)
   asm("" : "+s"(qi));
@@ -1460,8 +1461,7 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
       u64 x0[DNUM], x1[DNUM], kb0[DNUM], kb1[DNUM], ka0[DNUM], ka1[DNUM];
 #pragma unroll
       for (int d = 0; d < DNUM; ++d) {
-        const u64x2_t kb = *(const __attribute__((address_space(1))) u64x2_t*)(evk_b + (u64)d * rn + okey + e);
-        const u64x2_t ka = *(const __attribute__((address_space(1))) u64x2_t*)(evk_a + (u64)d * rn + okey + e);
+        const u64x2_t kb = kbv[e / 2][d], ka = kav[e / 2][d];
         const u32 p = cpos + e;
         x0[d] = lrow[d * G::RS + p + (p >> 4)];
         x1[d] = lrow[d * G::RS + (p + 1) + ((p + 1) >> 4)];
@@ -1498,8 +1498,7 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
     u128 s0[2] = {0, 0}, s1[2] = {0, 0};
 #pragma unroll
     for (int d = 0; d < DNUM; ++d) {
-      const u64x2_t kb = *(const __attribute__((address_space(1))) u64x2_t*)(evk_b + (u64)d * rn + okey + e);
-      const u64x2_t ka = *(const __attribute__((address_space(1))) u64x2_t*)(evk_a + (u64)d * rn + okey + e);
+      const u64x2_t kb = kbv[e / 2][d], ka = kav[e / 2][d];
       const u32 p = cpos + e;
       const u64 x0 = lrow[d * G::RS + p + (p >> 4)];
       const u64 x1 = lrow[d * G::RS + (p + 1) + ((p + 1) >> 4)];

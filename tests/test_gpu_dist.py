@@ -135,3 +135,41 @@ def test_keyswitch_dist_one_rank_rccl(fc, batch, chunks):
     assert len(ms) == dist_plan(L, log_n, 1, 0, batch, chunks).chunks
     assert all(v >= 0 for v in ms)
     comm.close()
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_bench_dist_check_native_world1(fc, chunks):
+    """bench.py's dist_check on the GPU (world 1): the native RCCL key-switch and the limb-sharded
+    HomMult against the single-device calls count zero mismatched words, and a corrupted shard is
+    counted -- the check that makes the driver's multi-GPU runs fail loudly on a wrong answer."""
+    import os
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from fhecore.dist import LimbShard, RcclComm
+
+    L, K, dnum, log_n = 16, 4, 4, 13
+    ctx = fc.Context(log_n, L=L, K=K, dnum=dnum)
+    comm = RcclComm()
+    shard = LimbShard(L, 1, 0)
+    d2 = fc.to_device(rand(ctx.moduli, log_n, (2 * chunks,), seed=11))
+    eb = fc.to_device(rand(ctx.all_moduli, log_n, (dnum,), seed=12))
+    ea = fc.to_device(rand(ctx.all_moduli, log_n, (dnum,), seed=13))
+    native = lambda d, kb, ka: ctx.keyswitch_dist(comm, d, kb, ka, chunks=chunks)  # noqa: E731
+    assert bench.check_keyswitch_shard(ctx, shard, K, d2, eb, ea, native) == 0
+
+    def corrupted(d, kb, ka):
+        k0, k1 = native(d, kb, ka)
+        k1.view(-1)[7] ^= 1
+        return k0, k1
+
+    assert bench.check_keyswitch_shard(ctx, shard, K, d2, eb, ea, corrupted) == 1
+    hctx = fc.Context(log_n, L=4)
+    a = fc.to_device(rand(hctx.moduli, log_n, (2, 2), seed=14))
+    b = fc.to_device(rand(hctx.moduli, log_n, (2, 2), seed=15))
+    assert bench.check_hommult_shard(hctx, LimbShard(4, 1, 0), a, b) == 0
+    torch.cuda.synchronize()
+    comm.close()

@@ -155,6 +155,36 @@ def main():
             out[f"ks N={G}{tag}"] = {"limbs_per_gpu": sh.nlimbs, "special_limbs_per_gpu": kk,
                                      "batch": B, "ms_per_batch": round(dk * 1e3, 4)}
             del eb, ea, d2, gat, ks0, ks1, ws
+    # the leg's chunking at N > 1 (fhe_keyswitch_dist: one call per chunk of the batch): rank 0's
+    # share of the whole batch issued as chunks of B / c ciphertexts, c = 1, 2, 4 -- the launch
+    # tails that more, smaller chunks cost against the gather time they let overlap
+    kctx = kctxs[K]
+    for G in (2, 4, 8):
+        sh = fdist.LimbShard(Lk, G, 0)
+        rows = sh.evk_rows(K)
+        allm = kctx.all_moduli
+        eb = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
+        ea = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
+        for c in (1, 2, 4):
+            cb = B // c
+            d2 = uniform_limbs(gen, kctx.moduli[sh.lo:sh.hi], (cb,), n)
+            gat = torch.zeros(G * cb * sh.width * n, dtype=torch.int64, device="cuda")
+            ks0 = kctx.empty(cb, sh.nlimbs, n)
+            ks1 = kctx.empty(cb, sh.nlimbs, n)
+            ws = kctx.workspace(lib.fhe_keyswitch_workspace(kctx.handle, sh.nlimbs, cb))
+
+            def chunked():
+                for _ in range(c):
+                    kctx.intt(d2, limb0=sh.lo)
+                    rc = lib.fhe_keyswitch_shard_ranked(
+                        kctx.handle, ks0.data_ptr(), ks1.data_ptr(), gat.data_ptr(), G,
+                        d2.data_ptr(), eb.data_ptr(), ea.data_ptr(), sh.lo, sh.nlimbs, cb,
+                        ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                    assert rc == 0, lib.fhe_last_error()
+
+            out.setdefault(f"ks N={G} chunked", {})[f"{c} chunk(s) of {cb}"] = round(
+                rate(chunked, 20, 50) * 1e3, 4)
+            del d2, gat, ks0, ks1, ws
     base = out["ks N=1"]["ms_per_batch"]
     for G in (1, 2, 4, 8):
         for tag in ("", " P-sharded proxy"):
