@@ -66,6 +66,9 @@ def parse():
                     help="hommult: skip the key-switch ride-along leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dist-check", action="store_true",
+                    help="skip the closing dist_check (profiling runs: its small launches would "
+                         "mix into the per-kernel averages)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="hommult: skip the live rocprofv3 traffic passes (roofline.traffic then "
                          "falls back to the committed profiles/hbm_traffic.json)")
@@ -428,9 +431,10 @@ def run_hommult(args, world, rank):
 
         out["keyswitch_leg"] = guarded_leg(ks_leg, out, rank, "keyswitch_leg")
     # after every timed leg: the sharded paths against each rank's single-device result
-    out["dist_check"] = guarded_leg(lambda: dist_check(world, rank, hm_ctx=ctx,
-                                                       ks_leg=legs.get("ks")),
-                                    out, rank, "dist_check")
+    if not args.no_dist_check:
+        out["dist_check"] = guarded_leg(lambda: dist_check(world, rank, hm_ctx=ctx,
+                                                           ks_leg=legs.get("ks")),
+                                        out, rank, "dist_check")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_hommult(ctx.moduli, args.log_n, args.cpu_seconds)
@@ -789,8 +793,9 @@ def run_keyswitch(args, world, rank):
     out.pop("warmup")
     out.pop("steps")
     out["scaling"] = out["config"].pop("scaling")
-    out["dist_check"] = guarded_leg(lambda: dist_check(world, rank, ks_leg=leg), out, rank,
-                                    "dist_check")
+    if not args.no_dist_check:
+        out["dist_check"] = guarded_leg(lambda: dist_check(world, rank, ks_leg=leg), out, rank,
+                                        "dist_check")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_keyswitch(leg.ctx.moduli, leg.ctx.special, args.log_n, leg.DNUM,
