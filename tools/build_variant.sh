@@ -2,13 +2,20 @@
 # Build an A/B variant of libfhecore with extra compiler defines into tools/variants/<name>.so
 # (for experiments: the shipped sources have no A/B switches left -- the measured alternatives are
 # recorded in DESIGN.md §8 -- so a variant means editing a copy of the sources or adding a define)
-# usage: tools/build_variant.sh name "-DFOO=1 -DBAR=2"
+# usage: tools/build_variant.sh name "-DFOO=1 -DBAR=2"   (REV=<git rev>: build that commit's sources,
+# e.g. REV=HEAD for the committed build against an edited working tree)
 set -e
 name=$1; defs=$2
 root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/tools/variants/$name; mkdir -p $out
+src=$root/gpu-fhe_amd/csrc
+if [ -n "$REV" ]; then
+  tmp=$(mktemp -d /tmp/fhe_rev_XXXX)
+  git -C "$root" archive "$REV" gpu-fhe_amd/csrc include | tar -x -C "$tmp"
+  src=$tmp/gpu-fhe_amd/csrc
+fi
 for f in host_tables.cpp context.cpp capi.cpp prof.cpp ntt.hip ntt_ks.hip elementwise.hip rns.hip galois.hip wire.cpp serialize.cpp pipeline.hip keygen.hip dist.cpp; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $defs -c $root/gpu-fhe_amd/csrc/$f -o $out/$f.o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $defs -c $src/$f -o $out/$f.o &
 done
 wait || exit 1
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $root/tools/variants/$name.so $out/*.o -L/opt/rocm/lib -lrccl
