@@ -14,10 +14,12 @@ if [ -n "$REV" ]; then
   git -C "$root" archive "$REV" gpu-fhe_amd/csrc include | tar -x -C "$tmp"
   src=$tmp/gpu-fhe_amd/csrc
 fi
+pids=()
 for f in host_tables.cpp context.cpp capi.cpp prof.cpp ntt.hip ntt_ks.hip elementwise.hip rns.hip galois.hip wire.cpp serialize.cpp pipeline.hip keygen.hip dist.cpp; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $defs -c $src/$f -o $out/$f.o &
+  pids+=($!)
 done
-wait || exit 1
+for p in "${pids[@]}"; do wait "$p" || exit 1; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $root/tools/variants/$name.so $out/*.o -L/opt/rocm/lib -lrccl
 rm -rf $out
 echo built tools/variants/$name.so
