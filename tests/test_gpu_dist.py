@@ -173,3 +173,25 @@ def test_bench_dist_check_native_world1(fc, chunks):
     assert bench.check_hommult_shard(hctx, LimbShard(4, 1, 0), a, b) == 0
     torch.cuda.synchronize()
     comm.close()
+
+
+def test_bench_default_line_end_to_end():
+    """bench.py as the driver runs it (one GPU, a short run): one JSON line carrying the headline,
+    the roofline, the key-switch leg and a bit-exact dist_check, and exit status 0."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup",
+                        "1", "--batch", "8", "--ks-batch", "8", "--no-cpu-baseline", "--no-pmc"],
+                       capture_output=True, text=True, timeout=110, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["value"] > 0 and line["unit"] == "HomMult/s" and line["n_gpus"] == 1
+    assert line["roofline"]["kernel"] == "hm_row_tensor" and line["roofline"]["frac"] > 0
+    assert line["keyswitch_leg"]["value"] > 0
+    assert line["dist_check"]["result"] == "bit-exact"
