@@ -24,6 +24,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -1062,7 +1063,7 @@ def dist_check(world, rank, hm_ctx=None, ks_leg=None, seed=4321):
 
 
 _EMIT = {"failed": []}  # json_fd, args, world (set by main); failed: reasons for a non-zero exit
-_EMIT_LOCK = None
+_EMIT_LOCK = threading.Lock()  # the main thread and a leg's watchdog may both try to print
 
 
 def failure_reasons(out):
@@ -1081,11 +1082,6 @@ def failure_reasons(out):
 def emit_line(out, cpu):
     """Rank 0's one JSON line on the saved stdout -- at most once per process, whichever thread
     (the main one or a leg's watchdog) gets there first."""
-    global _EMIT_LOCK
-    import threading
-
-    if _EMIT_LOCK is None:
-        _EMIT_LOCK = threading.Lock()
     with _EMIT_LOCK:
         if _EMIT.get("emitted"):
             return False
@@ -1116,7 +1112,6 @@ def guarded_leg(fn, out, rank, name, timeout_s=180.0):
     (main / conclude), and a leg still running after `timeout_s` (e.g. a collective that never
     completes on some node) makes rank 0 print the line without it and every rank exit
     EXIT_LEG_FAILED at once."""
-    import threading
 
     def fire():
         if rank == 0:
