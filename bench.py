@@ -226,14 +226,11 @@ def traffic_from_profile(kernel, shape):
                                      "and per-GPU shape")
 
 
-def measure_traffic_live(kernel_match, probe_args, timeout_s=150):
-    """HBM bytes per launch of the kernel whose name contains `kernel_match`, measured in this run:
-    two rocprofv3 passes (--pmc FETCH_SIZE, then --pmc WRITE_SIZE, one counter group each, no
-    tracing) over a child process that repeats the launch at the bench shape
-    (tools/hm_traffic_probe.py), corrected as MI355X_MICROARCH.md's HBM section prescribes and as
-    tools/pmc_traffic.sh calibrated on the column pass: read = 2 x FETCH_SIZE KiB, write =
-    WRITE_SIZE KiB.  The child is started as a new process (never exec), in its own session, and
-    killed with its group on timeout.  Returns (bytes, None) or (None, reason)."""
+def rocprof_pmc(counters, probe, probe_args, timeout_s=150):
+    """One `rocprofv3 --pmc <counters>` pass (no tracing) over a child process running
+    tools/<probe> with `probe_args`: the child is started as a new process (never exec), in its own
+    session, and killed with its group on timeout.  Returns (rows, stdout, None) -- rows of
+    (kernel name, counter, value) per dispatch -- or (None, None, reason)."""
     import csv
     import glob
     import shutil
@@ -243,39 +240,85 @@ def measure_traffic_live(kernel_match, probe_args, timeout_s=150):
     prof = shutil.which("rocprofv3") or (
         "/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
     if not prof:
-        return None, "rocprofv3 not found"
+        return None, None, "rocprofv3 not found"
     tmp = tempfile.mkdtemp(prefix="fhe_pmc_", dir="/tmp")
-    per = {}
     try:
-        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-            d = os.path.join(tmp, counter)
-            cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
-                   sys.executable, os.path.join(ROOT, "tools", "hm_traffic_probe.py"), *probe_args]
-            env = dict(os.environ, TMPDIR="/tmp")
-            proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
-                                    stderr=subprocess.DEVNULL, start_new_session=True)
-            try:
-                rc = proc.wait(timeout=timeout_s)
-            except subprocess.TimeoutExpired:
-                os.killpg(proc.pid, signal.SIGKILL)
-                proc.wait()
-                return None, f"rocprofv3 --pmc {counter} timed out after {timeout_s} s"
-            if rc != 0:
-                return None, f"rocprofv3 --pmc {counter} exited with {rc}"
-            vals = []
-            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-                with open(f) as fh:
-                    for r in csv.DictReader(fh):
-                        if kernel_match in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                            vals.append(float(r["Counter_Value"]))
-            if not vals:
-                return None, f"no {kernel_match} dispatch in the {counter} pass"
-            per[counter] = sum(vals) / len(vals)
+        cmd = [prof, "--pmc", *counters, "-d", tmp, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.join(ROOT, "tools", probe), *probe_args]
+        env = dict(os.environ, TMPDIR="/tmp")
+        proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE,
+                                stderr=subprocess.DEVNULL, start_new_session=True, text=True)
+        try:
+            out, _ = proc.communicate(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
+            proc.wait()
+            return None, None, f"rocprofv3 --pmc {' '.join(counters)} timed out after {timeout_s} s"
+        if proc.returncode != 0:
+            return None, None, f"rocprofv3 --pmc {' '.join(counters)} exited with {proc.returncode}"
+        rows = []
+        for f in glob.glob(os.path.join(tmp, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    rows.append((r["Kernel_Name"], r["Counter_Name"], float(r["Counter_Value"])))
+        return rows, out, None
     except (OSError, ValueError, KeyError) as e:
-        return None, f"traffic measurement failed: {e}"
+        return None, None, f"PMC pass failed: {e}"
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def measure_traffic_live(kernel_match, probe_args, timeout_s=150):
+    """HBM bytes per launch of the kernel whose name contains `kernel_match`, measured in this run:
+    two rocprofv3 passes (--pmc FETCH_SIZE, then --pmc WRITE_SIZE, one counter group each, no
+    tracing) over a child process that repeats the launch at the bench shape
+    (tools/hm_traffic_probe.py), corrected as MI355X_MICROARCH.md's HBM section prescribes and as
+    tools/pmc_traffic.sh calibrated on the column pass: read = 2 x FETCH_SIZE KiB, write =
+    WRITE_SIZE KiB.  Returns (bytes, None) or (None, reason)."""
+    per = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows, _, why = rocprof_pmc([counter], "hm_traffic_probe.py", probe_args, timeout_s)
+        if rows is None:
+            return None, why
+        vals = [v for k, c, v in rows if kernel_match in k and c == counter]
+        if not vals:
+            return None, f"no {kernel_match} dispatch in the {counter} pass"
+        per[counter] = sum(vals) / len(vals)
     return int(2 * 1024 * per["FETCH_SIZE"] + 1024 * per["WRITE_SIZE"]), None
+
+
+def measure_keyswitch_valu_live(log_n, batch, timeout_s=150):
+    """SQ_INSTS_VALU of one key-switch call at the leg's shape, measured in this run: one
+    `rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES` pass over tools/ks_valu_probe.py, which makes a few
+    fhe_keyswitch_dist calls and then runs the butterfly ceiling kernels (bfly_peak.hip) in the same
+    process.  Returns ({per-kernel VALU per call}, ceiling G VALU wave-instructions/s, None) or
+    (None, None, reason)."""
+    rows, out, why = rocprof_pmc(["SQ_INSTS_VALU", "SQ_WAVES"], "ks_valu_probe.py",
+                                 ["--log-n", str(log_n), "--batch", str(batch)], timeout_s)
+    if rows is None:
+        return None, None, why
+    try:
+        meta = json.loads(out.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return None, None, "ks_valu_probe printed no result line"
+    short = lambda k: k.replace("void fhe::(anonymous namespace)::", "").replace(  # noqa: E731
+        "void (anonymous namespace)::", "").split("(")[0]
+    tot, cnt = {}, {}
+    for k, c, v in rows:
+        if c != "SQ_INSTS_VALU":
+            continue
+        tot[short(k)] = tot.get(short(k), 0.0) + v
+        cnt[short(k)] = cnt.get(short(k), 0) + 1
+    ks = {k: v / meta["calls"] for k, v in tot.items()
+          if "fhe::" in k or (k.startswith("k_") and "bfly_peak" not in k)}
+    ceil = 0.0
+    for k, v in tot.items():
+        if k.startswith("k_bfly_peak"):
+            ms = meta["peak_ms_per_launch"]["inverse" if "<true>" in k else "forward"]
+            ceil = max(ceil, v / cnt[k] / (ms * 1e-3) / 1e9)
+    if not ks or not ceil:
+        return None, None, "no key-switch or ceiling dispatches in the PMC pass"
+    return ks, ceil, None
 
 
 def roofline(kernel, alg_bytes, ms, shape):
@@ -714,6 +757,7 @@ class KeyswitchLeg:
         self.B = args.ks_batch
         self.d2 = uniform_limbs(gen, ctx.moduli[self.shard.lo:self.shard.hi], (self.B,), n)
         self.chunks = args.ks_chunks or (1 if world == 1 else 4)
+        self.live_pmc = world == 1 and rank == 0 and not args.no_pmc
         # the native path needs one GPU per rank (RCCL refuses two ranks on one device); the
         # gloo rehearsal of several ranks on one GPU takes the torch.distributed form instead
         # (fhecore.dist.sharded_keyswitch: INTT, one all_gather through the host, local step)
@@ -765,24 +809,42 @@ class KeyswitchLeg:
             "keyswitch (whole, per GPU; NTT butterflies only)",
             (dnum * (nl + K) + nl) * full, (nl + 2 * K) * full, ms_per_ks)
         # ... and by VALU instruction issue, which counts everything the kernels execute (base
-        # conversion products, inner products, reductions, addressing): SQ_INSTS_VALU per launch
-        # of each key-switch kernel at this shape (committed rocprofv3 --pmc pass) over this run's
-        # time, against the issue rate of the butterfly ceiling kernel in that profiled process
+        # conversion products, inner products, reductions, addressing): SQ_INSTS_VALU of each
+        # key-switch kernel at this shape from a rocprofv3 --pmc pass over a child process
+        # (tools/ks_valu_probe.py), over this run's time, against the issue rate of the butterfly
+        # ceiling kernel in that profiled process.  Without the pass (--no-pmc, or it failed) the
+        # committed profile of the same shape stands in, and says so.
+        if world == 1:
+            res["roofline_valu"] = self.valu_roofline(dt / targs.steps)
+        return res
+
+    def valu_roofline(self, step_s):
+        why = "--no-pmc"
+        if self.live_pmc:
+            ks, ceil, why = measure_keyswitch_valu_live(self.log_n, self.B)
+            if ks is not None:
+                per_step = sum(ks.values())
+                ach = per_step / step_s / 1e9
+                return {"bound": "valu", "achieved": round(ach, 1), "peak": round(ceil, 2),
+                        "unit": "G VALU wave-instructions/s", "frac": round(ach / ceil, 4),
+                        "valu_instr_per_step": per_step,
+                        "valu_source": "measured in this run: rocprofv3 --pmc SQ_INSTS_VALU over "
+                                       "tools/ks_valu_probe.py (same shape; ceiling = "
+                                       "k_bfly_peak in that process); time from this run",
+                        "valu_instr_per_kernel": {k: round(v) for k, v in ks.items()}}
         prof, prof_path = valu_profile()
-        if prof and world == 1 and B == prof.get("shape", {}).get("batch"):
-            per_step = sum(v["valu_instr_per_launch"] * v["launches_per_step"]
-                           for k, v in prof["kernels"].items() if k.startswith("k_") and
-                           "bfly_peak" not in k)
-            ach = per_step / (dt / targs.steps) / 1e9
-            res["roofline_valu"] = {
-                "bound": "valu", "achieved": round(ach, 1), "peak": prof["ceiling_valu_g_per_s"],
-                "unit": "G VALU wave-instructions/s", "frac": round(ach / prof["ceiling_valu_g_per_s"], 4),
-                "valu_instr_per_step": per_step,
+        if not prof or self.B != prof.get("shape", {}).get("batch"):
+            return {"valu_live_error": why, "frac": None}
+        per_step = sum(v["valu_instr_per_launch"] * v["launches_per_step"]
+                       for k, v in prof["kernels"].items() if k.startswith("k_") and
+                       "bfly_peak" not in k)
+        ach = per_step / step_s / 1e9
+        return {"bound": "valu", "achieved": round(ach, 1), "peak": prof["ceiling_valu_g_per_s"],
+                "unit": "G VALU wave-instructions/s",
+                "frac": round(ach / prof["ceiling_valu_g_per_s"], 4),
+                "valu_instr_per_step": per_step, "valu_live_error": why,
                 "valu_source": f"committed, not measured in this run: {prof_path} "
-                               "(SQ_INSTS_VALU of every key-switch kernel, same shape); time from this run",
-                "per_kernel_frac_of_peak": {k: v.get("frac_of_bfly_peak_issue")
-                                            for k, v in prof["kernels"].items()
-                                            if k.startswith("k_") and "bfly_peak" not in k}}
+                               "(SQ_INSTS_VALU of every key-switch kernel, same shape); time from this run"}
         return res
 
 

@@ -166,3 +166,33 @@ def test_shard_mismatches_counts_only_own_limbs():
     got[0, 1, 0] -= 1
     assert bench.shard_mismatches(got, full, sh) == 2
     assert bench.shard_mismatches(torch.empty(2, 0, 8), full, LimbShard(4, 8, 7)) == 0
+
+
+def test_keyswitch_valu_live_parsing(monkeypatch):
+    """The live VALU pass: per-call VALU of the key-switch kernels (torch's own and the ceiling
+    kernel's excluded), and the ceiling = VALU per ceiling launch / that launch's own time."""
+    ns = "void fhe::(anonymous namespace)::"
+    rows = [(ns + "k_modup_col<16, 16, 4>(unsigned long*)", "SQ_INSTS_VALU", 100.0),
+            (ns + "k_modup_col<16, 16, 4>(unsigned long*)", "SQ_INSTS_VALU", 100.0),
+            (ns + "k_moddown_row<16, 16>(unsigned long*)", "SQ_INSTS_VALU", 50.0),
+            (ns + "k_moddown_row<16, 16>(unsigned long*)", "SQ_WAVES", 7.0),
+            ("void at::native::vectorized_elementwise_kernel<4>(int)", "SQ_INSTS_VALU", 1e9),
+            ("void (anonymous namespace)::k_bfly_peak<false>(unsigned long*)", "SQ_INSTS_VALU", 6e8),
+            ("void (anonymous namespace)::k_bfly_peak<false>(unsigned long*)", "SQ_INSTS_VALU", 6e8),
+            ("void (anonymous namespace)::k_bfly_peak<true>(unsigned long*)", "SQ_INSTS_VALU", 5e8)]
+    out = "noise\n" + json.dumps({"calls": 2, "batch": 32,
+                                  "peak_ms_per_launch": {"forward": 1.0, "inverse": 1.0}})
+    seen = {}
+
+    def fake(counters, probe, args, timeout_s=150):
+        seen.update(counters=counters, probe=probe, args=args)
+        return rows, out, None
+
+    monkeypatch.setattr(bench, "rocprof_pmc", fake)
+    ks, ceil, why = bench.measure_keyswitch_valu_live(16, 32)
+    assert why is None and seen["probe"] == "ks_valu_probe.py"
+    assert seen["args"] == ["--log-n", "16", "--batch", "32"]
+    assert ks == {"k_modup_col<16, 16, 4>": 100.0, "k_moddown_row<16, 16>": 25.0}
+    assert ceil == pytest.approx(600.0)  # 6e8 per 1 ms launch = 600 G/s
+    monkeypatch.setattr(bench, "rocprof_pmc", lambda *a, **k: (None, None, "timed out"))
+    assert bench.measure_keyswitch_valu_live(16, 32) == (None, None, "timed out")
