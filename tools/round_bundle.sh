@@ -4,8 +4,10 @@
 #      rocprofv3 bundle of the default command (tools/profile_round.sh: line, kernel-trace stats,
 #      FETCH_SIZE and WRITE_SIZE passes);
 #   B: every other workload's line (with its cpu_baseline), the key-switch kernel-trace stats and
-#      its SQ_INSTS_VALU passes (tools/kspmc.sh; summarise with tools/valu_roofline.py).
-# usage: tools/round_bundle.sh <out> A|B
+#      its SQ_INSTS_VALU passes (tools/kspmc.sh; summarise with tools/valu_roofline.py);
+#   R: the 2-rank rehearsal of the driver's multi-GPU launch on the box's one GPU (gloo: RCCL
+#      refuses two ranks on one device), with its dist_check.
+# usage: tools/round_bundle.sh <out> A|B|R
 set -o pipefail
 out=${1:-gpurun_out/bundle}; part=${2:-A}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p "$out"
@@ -14,6 +16,10 @@ if [ "$part" = A ]; then
   tail -n1 "$out/gputests.log"
   timeout -k 10 300 python3 bench.py --warmup 5 --steps 20 > "$out/bench_w5.json" 2> "$out/bench_w5.err" || exit $?
   bash tools/profile_round.sh "$out/hm" || exit $?
+elif [ "$part" = R ]; then
+  FHE_BENCH_BACKEND=gloo timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --warmup 5 --steps 20 \
+    > "$out/rehearsal_2rank.json" 2> "$out/rehearsal_2rank.err" || exit $?
 else
   for w in "keyswitch" "ntt" "vec" "mulrelin" "rotate" "ntt-batch --steps 5 --warmup 2"; do
     tag=$(echo $w | cut -d' ' -f1 | tr -d '-')
