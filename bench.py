@@ -436,6 +436,13 @@ def run_hommult(args, world, rank):
         "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
         "roofline": roofline(dom, alg, kavg.get(dom, float("nan")), shape),
     }
+    # algorithmic bytes exclude the twiddles (cache-resident), reported separately:
+    # the forward and inverse row tables of this rank's limbs, (w, w') pairs of 16 B, N per limb
+    tw = 2 * shard.nlimbs * n * 16
+    rf = out["roofline"]
+    rf["twiddle_bytes_per_launch"] = tw
+    rf["achieved_with_twiddles"] = round((alg + tw) / (rf["kernel_ms"] * 1e-3) / 1e9, 1)
+    rf["frac_with_twiddles"] = round(rf["achieved_with_twiddles"] / HBM_PEAK_GBPS, 4)
     # the fused row kernel is limited by VALU issue: its integer-ALU roofline, and
     # the same for the whole pipeline (7 full NTTs per ct x ct limb)
     units = gbatch * shard.nlimbs
@@ -457,7 +464,6 @@ def run_hommult(args, world, rank):
     if rank == 0 and world == 1 and not args.no_pmc and args.bits == 60:
         live, why = measure_traffic_live("k_hommult_row", [
             "--log-n", str(args.log_n), "--limbs", str(L), "--batch", str(gbatch)])
-        rf = out["roofline"]
         if live is not None:
             rf["traffic_committed"], rf["traffic"] = rf["traffic"], live
             rf["traffic_source"] = (
@@ -465,6 +471,7 @@ def run_hommult(args, world, rank):
                 "(separate) over tools/hm_traffic_probe.py at this shape, k_hommult_row mean per "
                 "dispatch; read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB (gfx950 correction)")
             rf["traffic_over_alg"] = round(live / alg, 4)
+            rf["traffic_over_alg_with_twiddles"] = round(live / (alg + tw), 4)
         else:
             rf["traffic_live_error"] = why
     legs = {}
