@@ -481,6 +481,13 @@ def run_hommult(args, world, rank):
             return legs["ks"].run(argparse.Namespace(warmup=20, steps=50))
 
         out["keyswitch_leg"] = guarded_leg(ks_leg, out, rank, "keyswitch_leg")
+        # the profiled child pass runs outside the watchdog: it has its own time limit, after
+        # which it is killed and the committed profile stands in
+        if "ks" in legs and "error" not in out["keyswitch_leg"] and world == 1:
+            try:
+                out["keyswitch_leg"]["roofline_valu"] = legs["ks"].valu_roofline()
+            except Exception as e:  # noqa: BLE001 -- a measurement, never a reason to fail the line
+                out["keyswitch_leg"]["roofline_valu"] = {"valu_live_error": repr(e), "frac": None}
     # after every timed leg: the sharded paths against each rank's single-device result
     if not args.no_dist_check:
         out["dist_check"] = guarded_leg(lambda: dist_check(world, rank, hm_ctx=ctx,
@@ -781,7 +788,7 @@ class KeyswitchLeg:
         else:
             fdist.sharded_keyswitch(self.ctx, self.d2, self.evk_b, self.evk_a, self.shard)
 
-    def run(self, targs):
+    def run(self, targs, valu=False):
         L, K, dnum, B, world = self.L, self.K, self.DNUM, self.B, self.world
         n = 1 << self.log_n
         dt, kavg = timed(self.step, targs, world, 64 * targs.steps + 64)
@@ -821,11 +828,13 @@ class KeyswitchLeg:
         # (tools/ks_valu_probe.py), over this run's time, against the issue rate of the butterfly
         # ceiling kernel in that profiled process.  Without the pass (--no-pmc, or it failed) the
         # committed profile of the same shape stands in, and says so.
-        if world == 1:
-            res["roofline_valu"] = self.valu_roofline(dt / targs.steps)
+        self.step_s = dt / targs.steps
+        if world == 1 and valu:
+            res["roofline_valu"] = self.valu_roofline()
         return res
 
-    def valu_roofline(self, step_s):
+    def valu_roofline(self):
+        step_s = self.step_s
         why = "--no-pmc"
         if self.live_pmc:
             ks, ceil, why = measure_keyswitch_valu_live(self.log_n, self.B)
@@ -857,7 +866,7 @@ class KeyswitchLeg:
 
 def run_keyswitch(args, world, rank):
     leg = KeyswitchLeg(args, world, rank)
-    out = leg.run(args)
+    out = leg.run(args, valu=True)
     out["metric"] = ("key-switches/sec at N=2^16, L=16, K=4, dnum=4 (RNS limbs sharded, RCCL "
                      "all-gather)")
     out.pop("warmup")
