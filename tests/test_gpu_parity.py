@@ -433,3 +433,30 @@ def test_lazy_headroom_variants_match_oracle(fc, bits):
     d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b)))
     for i in range(2):
         assert (d[i] == coracle.hommult(a[i], b[i], mods)).all()
+
+
+def test_keyswitch_batch_in_cache_sized_passes(fc):
+    """fhe_keyswitch runs a batch above 256 MiB of d2 in passes (N = 2^16, L = 16: 32 ciphertexts
+    per pass): 33 ciphertexts = a full pass + a one-ciphertext pass.  The whole batch equals the
+    one-pass distributed path (fhe_keyswitch_dist, one rank, one chunk) word for word, and the
+    first and last ciphertexts equal the C oracle."""
+    from fhecore.dist import RcclComm
+
+    L, K, dnum, B = 16, 4, 4, 33
+    ctx = ctx_for(fc, 16, L, K=K, dnum=dnum)
+    allm = ctx.all_moduli
+    d2 = rand(ctx.moduli, 16, (B,), seed=90)
+    eb = rand(allm, 16, (dnum,), seed=91)
+    ea = rand(allm, 16, (dnum,), seed=92)
+    dd, db, da = fc.to_device(d2), fc.to_device(eb), fc.to_device(ea)
+    ks0, ks1 = ctx.keyswitch(dd, db, da)
+    comm = RcclComm()
+    try:
+        w0, w1 = ctx.keyswitch_dist(comm, dd, db, da, chunks=1)
+    finally:
+        comm.close()
+    h0, h1 = fc.to_host(ks0), fc.to_host(ks1)
+    assert (h0 == fc.to_host(w0)).all() and (h1 == fc.to_host(w1)).all()
+    for b in (0, B - 1):
+        r0, r1 = coracle.keyswitch(d2[b], eb, ea, ctx.moduli, ctx.special, dnum)
+        assert (h0[b] == r0).all() and (h1[b] == r1).all(), b
