@@ -280,13 +280,14 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
   if ((rc = ensure_ws(ctx, dist_workspace(ctx, p, p.nlimbs), &ws, s))) return rc;
   u64* gather = static_cast<u64*>(ws);  // [nc][G][cb][cw][N]
   void* kws = gather + p.gather_words;
-  // 1 + 2: every chunk's INTT into its send block, then its gather on the comm stream.  With one
+  // 1 + 2: a chunk's INTT into its send block, then its gather on the comm stream.  With one
   // chunk nothing could overlap the gather, so it runs on the caller's stream: a cross-stream
   // event hand-off costs ~40 us of idle GPU per call (measured).
   const bool own_stream = p.chunks > 1;
   const hipStream_t gs = own_stream ? comm->stream : s;
-  for (u32 k = 0; k < p.chunks; ++k) {
-    if ((rc = dist_intt_chunk(ctx, p, k, d2_own, gather, s))) return rc;
+  auto issue = [&](u32 k) -> int {
+    int r;
+    if ((r = dist_intt_chunk(ctx, p, k, d2_own, gather, s))) return r;
     u64* gbuf = gather + (u64)k * p.ranks * p.block_words;
     if (own_stream) {
       FHE_HIP_CHECK(hipEventRecord(comm->ev_intt[k], s));
@@ -297,15 +298,22 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
                                  ncclUint64, comm->nccl, gs));
     FHE_HIP_CHECK(hipEventRecord(comm->ev_g1[k], gs));
     if (own_stream) FHE_HIP_CHECK(hipEventRecord(comm->ev_gather[k], gs));
-  }
-  comm->last_chunks = p.chunks;
-  prof_mark(s, "ks_dist_intt");
-  // 3: each chunk's key-switch once its gather has landed
+    return kOk;
+  };
+  // 3: chunk k's key-switch once its gather has landed, with chunk k + 1's INTT queued just
+  // before it (its gather overlaps this key-switch) and no further: only two chunks of gathered
+  // d2 are live at a time, so ModUp reads its sources from the Infinity Cache the gather just
+  // wrote instead of from HBM (all INTTs first left every chunk but the last evicted once the
+  // gathered batch outgrew the cache: DESIGN.md §8)
+  if ((rc = issue(0))) return rc;
   for (u32 k = 0; k < p.chunks; ++k) {
+    if (k + 1 < p.chunks && (rc = issue(k + 1))) return rc;
+    if (k == 0) prof_mark(s, "ks_dist_intt");
     if (own_stream) FHE_HIP_CHECK(hipStreamWaitEvent(s, comm->ev_gather[k], 0));
     if ((rc = dist_ks_chunk(ctx, p, k, ks0, ks1, d2_own, evk_b, evk_a, gather, kws, s)))
       return rc;
   }
+  comm->last_chunks = p.chunks;
   return kOk;
 }
 
