@@ -7,10 +7,11 @@
 //   2. one ncclAllGather (in place) of the coefficient-form d2 -> [G][chunk][c][N] on every rank;
 //   3. ModUp / NTT / inner product / ModDown of the rank's limbs (launch_keyswitch_shard, reading
 //      the rank-major gather layout directly: CAll::ranked -- no reorder copy).
-// The batch is split into chunks: the INTTs of every chunk are queued first on the caller's
-// stream, each chunk's all-gather runs on the communicator's own stream as soon as its INTT is
-// done, and the caller's stream waits for a chunk's gather only right before its key-switch, so
-// chunk k + 1's transfer overlaps chunk k's key-switch.
+// The batch is split into chunks: chunk k + 1's INTT is queued on the caller's stream right
+// before chunk k's key-switch, its all-gather runs on the communicator's own stream as soon as
+// that INTT is done, and the caller's stream waits for a chunk's gather only right before its
+// key-switch, so chunk k + 1's transfer overlaps chunk k's key-switch (and at most two chunks of
+// gathered d2 are live, which keeps ModUp's sources in the Infinity Cache).
 // Every offset comes from one host-side plan (fhe_dist_plan_*, exported so that the CPU suite
 // checks it for G = 1..8 without a GPU), and fhe_keyswitch_dist_loopback runs the same plan and
 // the same per-chunk steps for G virtual ranks on one device (the GPU suite's G > 1 path).
