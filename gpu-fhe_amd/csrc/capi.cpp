@@ -289,12 +289,6 @@ int fhe_keyswitch_shard(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const ui
                                 ws, hs(s));
 }
 
-// The single-device key-switch runs in passes of at most this many bytes of INTT(d2), the size of
-// the Infinity Cache: ModUp then reads its sources from the cache the INTT just wrote.  Measured
-// at N = 2^16, L = 16 (8 MiB of d2 per ciphertext): ModUp 16.2 us per ciphertext up to batch 32,
-// 19-21 us at 40-64, every other kernel linear in the batch.
-constexpr size_t kKsPassBytes = 256ull << 20;
-
 int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t* d2,
                   const uint64_t* evk_b, const uint64_t* evk_a, uint32_t batch, void* ws,
                   fhe_stream_t s) {
@@ -302,8 +296,7 @@ int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t
   if (rc) return rc;
   if (batch == 0) return kOk;
   const uint64_t ct_words = (uint64_t)c->L * c->n;
-  const uint32_t pass = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>(batch, kKsPassBytes / (ct_words * sizeof(uint64_t))));
+  const uint32_t pass = ks_pass_batch(c, batch);  // Infinity-Cache-sized passes
   const size_t bytes = keyswitch_workspace_bytes(c, c->L, pass);
   if ((rc = ensure_ws(c, bytes, &ws, hs(s)))) return rc;
   // c_all = INTT(d2) of one pass lives at the tail of the workspace (out of place: no copy of d2)
@@ -365,7 +358,7 @@ int fhe_rotate(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t gal
     set_error("fhe_rotate: out must not alias in");
     return kInvalid;
   }
-  if ((rc = ensure_ws(c, rotate_workspace_bytes(c, batch), &ws, hs(s)))) return rc;
+  if ((rc = ensure_ws(c, rotate_workspace_bytes(c, ks_pass_batch(c, batch)), &ws, hs(s)))) return rc;
   return launch_rotate(c, out, in, galois_elt, rot_b, rot_a, batch, ws, hs(s));
 }
 
@@ -406,7 +399,7 @@ int fhe_mul_relin(const fhe_ctx* c, uint64_t* out, const uint64_t* a, const uint
                   void* ws, fhe_stream_t s) {
   int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_mul_relin");
   if (rc) return rc;
-  if ((rc = ensure_ws(c, mul_relin_workspace_bytes(c, batch), &ws, hs(s)))) return rc;
+  if ((rc = ensure_ws(c, mul_relin_workspace_bytes(c, ks_pass_batch(c, batch)), &ws, hs(s)))) return rc;
   return launch_mul_relin(c, out, a, b, evk_b, evk_a, batch, rescale != 0, ws, hs(s));
 }
 

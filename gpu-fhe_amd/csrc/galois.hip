@@ -217,6 +217,15 @@ int launch_rotate(const fhe_ctx* c, u64* out, const u64* in, u32 galois_elt, con
   if (batch == 0) return kOk;
   const u32 L = c->L;
   const u64 n = c->n, ln = (u64)L * n;
+  // Infinity-Cache-sized passes (ks_pass_batch), each in the front of the workspace
+  if (const u32 pass = ks_pass_batch(c, batch); pass < batch) {
+    for (u32 b0 = 0; b0 < batch; b0 += pass) {
+      if (int rc = launch_rotate(c, out + b0 * 2 * ln, in + b0 * 2 * ln, galois_elt, rot_b, rot_a,
+                                 std::min(pass, batch - b0), ws, s))
+        return rc;
+    }
+    return kOk;
+  }
   u64* sc1 = static_cast<u64*>(ws);  // [batch][L][N]
   u64* sc0 = sc1 + batch * ln;
   u64* kws = sc0 + batch * ln;

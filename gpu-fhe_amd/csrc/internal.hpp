@@ -1,5 +1,6 @@
 // Library-internal context and launcher declarations for libfhecore (not installed).
 #pragma once
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -255,6 +256,17 @@ inline bool ks_prepared(const fhe_ctx* c) {
 // residues (dot_wide61 on 32-bit halves); the others read Sum30's 30-bit pieces (split30), which
 // the INTTs and k_modup_scale feeding them emit directly.
 inline bool ks_split30(const fhe_ctx* c) { return !c->lz16; }
+
+// The single-device key-switch paths (fhe_keyswitch, mul-relin, rotate) run a batch in passes of
+// at most this many bytes of INTT(d2), the size of the Infinity Cache: ModUp then reads its
+// sources from the cache the INTT just wrote.  Measured at N = 2^16, L = 16 (8 MiB of d2 per
+// ciphertext): ModUp 16.2 us per ciphertext up to batch 32, 19-21 us at 40-64, every other kernel
+// linear in the batch.
+constexpr size_t kKsPassBytes = 256ull << 20;
+inline uint32_t ks_pass_batch(const fhe_ctx* c, uint32_t batch) {
+  const uint64_t per = (uint64_t)c->L * c->n * sizeof(uint64_t);
+  return batch ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(batch, kKsPassBytes / per)) : 0;
+}
 int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& call,
                            const u64* d2_own, const u64* evk_b, const u64* evk_a, u32 limb0,
                            u32 nlimbs, u32 batch, void* ws, hipStream_t s,

@@ -65,6 +65,16 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   if (batch == 0) return kOk;
   const u32 L = c->L;
   const u64 n = c->n, ln = (u64)L * n;
+  // Infinity-Cache-sized passes (ks_pass_batch), each in the front of the workspace
+  if (const u32 pass = ks_pass_batch(c, batch); pass < batch) {
+    const u64 out_bs = 2 * (u64)(rescale ? L - 1 : L) * n;
+    for (u32 b0 = 0; b0 < batch; b0 += pass) {
+      if (int rc = launch_mul_relin(c, out + b0 * out_bs, a + b0 * 2 * ln, b + b0 * 2 * ln, evk_b,
+                                    evk_a, std::min(pass, batch - b0), rescale, ws, s))
+        return rc;
+    }
+    return kOk;
+  }
   u64* d = static_cast<u64*>(ws);        // [batch][2][L][N]: d0, d1
   u64* rl = d + 2 * batch * ln;          // [batch][2][L][N] relinearised, before the rescale
   u64* rws = rl + 2 * batch * ln;        // rescale workspace

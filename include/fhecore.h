@@ -139,9 +139,9 @@ int fhe_baseconv(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t
  * d2_own [batch][nlimbs][N] NTT form of Q-limbs [limb0, limb0 + nlimbs), evk slices
  * [dnum][nlimbs + K][N] (own Q-limbs then all K P-limbs); outputs [batch][nlimbs][N].  The
  * sharded outputs of G ranks concatenate to the single-device result bit for bit.
- * fhe_keyswitch runs the batch in passes of at most 256 MiB of d2 (the Infinity Cache), so its
- * internal workspace is sized for one pass; a caller's workspace of
- * fhe_keyswitch_workspace(ctx, L, batch) bytes is always large enough. */
+ * fhe_keyswitch (and fhe_mul_relin, fhe_rotate) run the batch in passes of at most 256 MiB of
+ * d2 (the Infinity Cache), so the internal workspace is sized for one pass; a caller's workspace
+ * of the documented *_workspace(ctx, ..., batch) bytes is always large enough. */
 size_t fhe_keyswitch_workspace(const fhe_ctx* ctx, uint32_t nlimbs, uint32_t batch);
 int fhe_keyswitch(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const uint64_t* d2,
                   const uint64_t* evk_b, const uint64_t* evk_a, uint32_t batch, void* workspace,

@@ -238,3 +238,30 @@ def test_rotate_hoisted_batch_matches_single_and_errors(fc):
     rc = lib.fhe_rotate_hoisted(ctx.handle, out.data_ptr(), ctd.data_ptr(), g_arr, b_arr, a_arr,
                                 2, 3, None, None)
     assert rc == -1 and b"null key pointer" in lib.fhe_last_error()
+
+
+def test_rotate_and_mul_relin_in_cache_sized_passes(fc):
+    """fhe_rotate and fhe_mul_relin run a batch above 256 MiB of d2 in passes (N = 2^16, L = 16:
+    32 ciphertexts per pass): 33 ciphertexts, each one equal to its own single-ciphertext call
+    (ciphertexts 0 and 31 in the first pass, 32 alone in the second)."""
+    import torch
+
+    log_n, L, K, dnum, B = 16, 16, 4, 4, 33
+    ctx = fc.Context(log_n, L=L, K=K, dnum=dnum)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(33)
+
+    def rows(mods, lead):
+        return torch.stack([torch.randint(0, q, lead + (1 << log_n,), generator=gen,
+                                          dtype=torch.int64, device="cuda") for q in mods], len(lead))
+
+    ct = rows(ctx.moduli, (B, 2))
+    ct2 = rows(ctx.moduli, (B, 2))
+    kb, ka = rows(ctx.all_moduli, (dnum,)), rows(ctx.all_moduli, (dnum,))
+    k = ctx.galois_elt(3)
+    rot = ctx.rotate(ct, k, kb, ka)
+    mr = ctx.mul_relin(ct, ct2, kb, ka, rescale=True)
+    for b in (0, 31, 32):
+        assert torch.equal(ctx.rotate(ct[b:b + 1], k, kb, ka), rot[b:b + 1]), b
+        assert torch.equal(ctx.mul_relin(ct[b:b + 1], ct2[b:b + 1], kb, ka, rescale=True),
+                           mr[b:b + 1]), b
