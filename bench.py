@@ -851,9 +851,12 @@ class KeyswitchLeg:
         prof, prof_path = valu_profile()
         if not prof or self.B != prof.get("shape", {}).get("batch"):
             return {"valu_live_error": why, "frac": None}
-        per_step = sum(v["valu_instr_per_launch"] * v["launches_per_step"]
-                       for k, v in prof["kernels"].items() if k.startswith("k_") and
-                       "bfly_peak" not in k)
+        try:
+            per_step = sum(v["valu_instr_per_launch"] * v["launches_per_step"]
+                           for k, v in prof["kernels"].items() if k.startswith("k_") and
+                           "bfly_peak" not in k)
+        except (KeyError, TypeError):
+            return {"valu_live_error": f"{why}; {prof_path} lacks per-step counts", "frac": None}
         ach = per_step / step_s / 1e9
         return {"bound": "valu", "achieved": round(ach, 1), "peak": prof["ceiling_valu_g_per_s"],
                 "unit": "G VALU wave-instructions/s",
