@@ -53,7 +53,8 @@ def parse():
                     default="hommult")
     ap.add_argument("--batch", type=int, default=None,
                     help="ciphertexts per GPU per step (default 64 for hommult -- the throughput "
-                         "batch: +3.5 %% over 16, fewer launch tails -- and 16 for the others)")
+                         "batch: +3.5 %% over 16, fewer launch tails --, 32 for mulrelin and rotate "
+                         "-- the key-switch's best batch -- and 16 for the others)")
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--bits", type=int, default=60, choices=[60, 61, 62, 63],
                     help="hommult: modulus chain of the largest primes below 2^bits (62, 63: the "
@@ -1238,7 +1239,9 @@ def main():
     if args.workload == "keyswitch" and args.batch is not None:
         args.ks_batch = args.batch
     if args.batch is None:
-        args.batch = 64 if args.workload == "hommult" else 16
+        # mul-relin and rotate at the key-switch's best batch (32: profiles/r04_ks_batch_sweep.txt,
+        # r04_mulrelin_rotate_batch_ab.txt: +2 % / +4 % over 16)
+        args.batch = {"hommult": 64, "mulrelin": 32, "rotate": 32}.get(args.workload, 16)
     world, rank = dist_setup(args)
     _EMIT.update(json_fd=json_fd, args=args, world=world)
     run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch, "vec": run_vec,
