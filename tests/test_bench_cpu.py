@@ -196,3 +196,21 @@ def test_keyswitch_valu_live_parsing(monkeypatch):
     assert ceil == pytest.approx(600.0)  # 6e8 per 1 ms launch = 600 G/s
     monkeypatch.setattr(bench, "rocprof_pmc", lambda *a, **k: (None, None, "timed out"))
     assert bench.measure_keyswitch_valu_live(16, 32) == (None, None, "timed out")
+
+
+def test_keyswitch_valu_fallback_reads_committed_profile(monkeypatch):
+    """Without the live pass (--no-pmc) the key-switch VALU roofline comes from the newest committed
+    profiles/rNN_keyswitch_pmc.json, which must carry per-step counts for the leg's batch; a failed
+    live pass falls back the same way and says why."""
+    from types import SimpleNamespace
+
+    leg = SimpleNamespace(live_pmc=False, B=32, step_s=2.0e-3, log_n=16)
+    r = bench.KeyswitchLeg.valu_roofline(leg)
+    assert r["frac"] is not None and 0.2 < r["frac"] < 1.5, r
+    assert r["valu_source"].startswith("committed") and r["valu_live_error"] == "--no-pmc"
+    monkeypatch.setattr(bench, "measure_keyswitch_valu_live", lambda *a: (None, None, "timed out"))
+    leg.live_pmc = True
+    r = bench.KeyswitchLeg.valu_roofline(leg)
+    assert r["valu_live_error"] == "timed out" and r["frac"] is not None
+    leg.B = 7  # no committed profile of that batch
+    assert bench.KeyswitchLeg.valu_roofline(leg)["frac"] is None
