@@ -227,17 +227,40 @@ def traffic_from_profile(kernel, shape):
                                      "and per-GPU shape")
 
 
+def profiled_parent(environ=None):
+    """Why this process runs under a profiler, or None.  rocprofv3 starts its target with the
+    rocprofiler-sdk tool library in LD_PRELOAD and its settings in ROCPROF* / ROCP_* variables;
+    that library initialises the GPU before the target's first line runs.  A nested rocprofv3
+    started from such a process inherits the preload, so its own launcher has initialised the GPU
+    when it execs the probe -- an exec the GPU box refuses (round 4: tools/kspmc.sh profiled
+    bench.py, whose live PMC passes then exited 126)."""
+    env = os.environ if environ is None else environ
+    if "rocprof" in env.get("LD_PRELOAD", ""):
+        return "LD_PRELOAD names the rocprofiler tool library"
+    keys = sorted(k for k in env if k.startswith(("ROCPROF", "ROCP_")))
+    if keys:
+        return f"rocprofiler environment present ({keys[0]})"
+    return None
+
+
 def rocprof_pmc(counters, probe, probe_args, timeout_s=150):
     """One `rocprofv3 --pmc <counters>` pass (no tracing) over a child process running
-    tools/<probe> with `probe_args`: the child is started as a new process (never exec), in its own
-    session, and killed with its group on timeout.  Returns (rows, stdout, None) -- rows of
-    (kernel name, counter, value) per dispatch -- or (None, None, reason)."""
+    tools/<probe> with `probe_args`: the child is started with Popen in its own session and killed
+    with its group on timeout.  rocprofv3's launcher then execs the probe's interpreter, which is
+    only safe while nothing in that launcher has touched the GPU: when this process itself runs
+    under a profiler (profiled_parent), the launcher would inherit the profiler's preload, so the
+    pass is skipped without starting anything.  Returns (rows, stdout, None) -- rows of (kernel
+    name, counter, value) per dispatch -- or (None, None, reason)."""
     import csv
     import glob
     import shutil
     import signal
     import subprocess
     import tempfile
+    nested = profiled_parent()
+    if nested:
+        return None, None, f"skipped: this process runs under a profiler ({nested}); a nested " \
+                           "rocprofv3 would exec its target after the GPU was initialised"
     prof = shutil.which("rocprofv3") or (
         "/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
     if not prof:
@@ -288,14 +311,15 @@ def measure_traffic_live(kernel_match, probe_args, timeout_s=150):
     return int(2 * 1024 * per["FETCH_SIZE"] + 1024 * per["WRITE_SIZE"]), None
 
 
-def measure_keyswitch_valu_live(log_n, batch, timeout_s=150):
-    """SQ_INSTS_VALU of one key-switch call at the leg's shape, measured in this run: one
+def measure_keyswitch_valu_live(log_n, batch, chunks=1, timeout_s=150):
+    """SQ_INSTS_VALU of one key-switch call at the leg's shape and chunking, measured in this run: one
     `rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES` pass over tools/ks_valu_probe.py, which makes a few
     fhe_keyswitch_dist calls and then runs the butterfly ceiling kernels (bfly_peak.hip) in the same
     process.  Returns ({per-kernel VALU per call}, ceiling G VALU wave-instructions/s, None) or
     (None, None, reason)."""
     rows, out, why = rocprof_pmc(["SQ_INSTS_VALU", "SQ_WAVES"], "ks_valu_probe.py",
-                                 ["--log-n", str(log_n), "--batch", str(batch)], timeout_s)
+                                 ["--log-n", str(log_n), "--batch", str(batch),
+                                  "--chunks", str(chunks)], timeout_s)
     if rows is None:
         return None, None, why
     try:
@@ -838,7 +862,7 @@ class KeyswitchLeg:
         step_s = self.step_s
         why = "--no-pmc"
         if self.live_pmc:
-            ks, ceil, why = measure_keyswitch_valu_live(self.log_n, self.B)
+            ks, ceil, why = measure_keyswitch_valu_live(self.log_n, self.B, self.chunks)
             if ks is not None:
                 per_step = sum(ks.values())
                 ach = per_step / step_s / 1e9
@@ -850,7 +874,8 @@ class KeyswitchLeg:
                                        "k_bfly_peak in that process); time from this run",
                         "valu_instr_per_kernel": {k: round(v) for k, v in ks.items()}}
         prof, prof_path = valu_profile()
-        if not prof or self.B != prof.get("shape", {}).get("batch"):
+        shape = (prof or {}).get("shape", {})
+        if not prof or self.B != shape.get("batch") or self.chunks != shape.get("chunks", 1):
             return {"valu_live_error": why, "frac": None}
         try:
             per_step = sum(v["valu_instr_per_launch"] * v["launches_per_step"]
@@ -865,7 +890,6 @@ class KeyswitchLeg:
                 "valu_instr_per_step": per_step, "valu_live_error": why,
                 "valu_source": f"committed, not measured in this run: {prof_path} "
                                "(SQ_INSTS_VALU of every key-switch kernel, same shape); time from this run"}
-        return res
 
 
 def run_keyswitch(args, world, rank):

@@ -191,7 +191,7 @@ def test_keyswitch_valu_live_parsing(monkeypatch):
     monkeypatch.setattr(bench, "rocprof_pmc", fake)
     ks, ceil, why = bench.measure_keyswitch_valu_live(16, 32)
     assert why is None and seen["probe"] == "ks_valu_probe.py"
-    assert seen["args"] == ["--log-n", "16", "--batch", "32"]
+    assert seen["args"] == ["--log-n", "16", "--batch", "32", "--chunks", "1"]
     assert ks == {"k_modup_col<16, 16, 4>": 100.0, "k_moddown_row<16, 16>": 25.0}
     assert ceil == pytest.approx(600.0)  # 6e8 per 1 ms launch = 600 G/s
     monkeypatch.setattr(bench, "rocprof_pmc", lambda *a, **k: (None, None, "timed out"))
@@ -204,7 +204,7 @@ def test_keyswitch_valu_fallback_reads_committed_profile(monkeypatch):
     live pass falls back the same way and says why."""
     from types import SimpleNamespace
 
-    leg = SimpleNamespace(live_pmc=False, B=32, step_s=2.0e-3, log_n=16)
+    leg = SimpleNamespace(live_pmc=False, B=32, chunks=1, step_s=2.0e-3, log_n=16)
     r = bench.KeyswitchLeg.valu_roofline(leg)
     assert r["frac"] is not None and 0.2 < r["frac"] < 1.5, r
     assert r["valu_source"].startswith("committed") and r["valu_live_error"] == "--no-pmc"
@@ -214,3 +214,33 @@ def test_keyswitch_valu_fallback_reads_committed_profile(monkeypatch):
     assert r["valu_live_error"] == "timed out" and r["frac"] is not None
     leg.B = 7  # no committed profile of that batch
     assert bench.KeyswitchLeg.valu_roofline(leg)["frac"] is None
+    leg.B, leg.chunks = 32, 4  # nor of that launch layout
+    assert bench.KeyswitchLeg.valu_roofline(leg)["frac"] is None
+
+
+def test_rocprof_pmc_skips_under_a_profiler(monkeypatch):
+    """Under a profiler (the rocprofiler tool library in LD_PRELOAD, or its ROCPROF* / ROCP_*
+    settings) a nested rocprofv3 would exec its target after its launcher initialised the GPU --
+    refused on the GPU box (round 4, tools/kspmc.sh).  rocprof_pmc must then return the reason
+    without starting any process."""
+    import subprocess
+
+    def no_popen(*a, **k):
+        raise AssertionError("rocprof_pmc started a process under a profiler")
+
+    monkeypatch.setattr(subprocess, "Popen", no_popen)
+    for var, val in (("LD_PRELOAD", "/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so"),
+                     ("ROCPROF_OUTPUT_PATH", "/tmp/x"), ("ROCP_TOOL_LIBRARIES", "x.so")):
+        for k in [k for k in os.environ if k.startswith(("ROCPROF", "ROCP_"))]:
+            monkeypatch.delenv(k)
+        monkeypatch.delenv("LD_PRELOAD", raising=False)
+        monkeypatch.setenv(var, val)
+        assert bench.profiled_parent() is not None
+        rows, out, why = bench.rocprof_pmc(["SQ_WAVES"], "ks_valu_probe.py", [])
+        assert rows is None and out is None and why.startswith("skipped: this process runs under")
+        # and the live measurements built on it report the skip instead of a number
+        ks, ceil, why2 = bench.measure_keyswitch_valu_live(16, 32)
+        assert ks is None and why2 == why
+        live, why3 = bench.measure_traffic_live("k_hommult_row", [])
+        assert live is None and why3 == why
+    assert bench.profiled_parent({"LD_PRELOAD": "/usr/lib/libother.so", "PATH": "/bin"}) is None

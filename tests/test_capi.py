@@ -99,6 +99,26 @@ def test_no_cpu_fallback_without_device():
         arithmetic.vec_add(np.zeros(4, np.uint64), np.zeros(4, np.uint64), 7)
     with pytest.raises(fhecore.FheError):
         arithmetic.NTT(np.zeros(4096, np.uint64))
+    # the reference's own import line reaches the same (HIP-only) path
+    import importlib
+
+    poly = importlib.import_module(" polynomial")
+    with pytest.raises(fhecore.FheError):
+        poly.poly_add((np.zeros(4, np.uint64),), (np.zeros(4, np.uint64),), 7)
+
+
+def test_reference_module_names_importable():
+    """`importlib.import_module(" polynomial")` -- the reference's module name, leading space
+    included (/root/reference/ polynomial.py) -- resolves to this package's drop-in and exports
+    the reference's names through the same star-import chain."""
+    import importlib
+
+    poly = importlib.import_module(" polynomial")
+    import polynomial
+
+    assert poly.poly_add is polynomial.poly_add
+    for name in ("vec_add", "vec_sub", "vec_mul", "NTT", "iNTT", "XXX", "np"):
+        assert hasattr(poly, name), name
 
 
 def test_keygen_seed_defaults_to_fresh_nonce():

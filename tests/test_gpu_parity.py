@@ -171,6 +171,25 @@ def test_reference_shim_ntt_and_poly_add(fc):
     assert isinstance(r, tuple) and (r[0] == v["add"]).all() and (r[1] == v["add"]).all()
 
 
+def test_reference_import_line_unchanged(fc):
+    """The reference's caller line, verbatim: importlib.import_module(" polynomial") with
+    gpu-fhe_amd/ on sys.path (/root/reference/ polynomial.py:1-5) gets this package's module, whose
+    poly_add runs on the HIP path and matches the reference-made vec_N4096_L1 fixture."""
+    import importlib
+
+    import fhecore
+
+    poly = importlib.import_module(" polynomial")
+    assert os.path.dirname(os.path.abspath(poly.__file__)) == os.path.dirname(
+        os.path.abspath(fhecore.__path__[0]))
+    v = np.load(os.path.join(GOLDEN, "vec_N4096_L1.npz"))
+    col = v["moduli"].reshape(-1, 1)
+    r = poly.poly_add((v["a"], v["b"]), (v["b"], v["a"]), col)
+    assert isinstance(r, tuple) and len(r) == 2
+    assert (r[0] == v["add"]).all() and (r[1] == v["add"]).all()
+    assert bool(v["ref_poly_add_returns_none"])  # the reference's own return (divergence)
+
+
 # ------------------------------------------------------------------------------- HomMult
 
 @pytest.mark.parametrize("fx", ["hommult_N4096_L2.npz", "hommult_N2048_L8_chain16.npz"])

@@ -1,11 +1,11 @@
 """The profiled command of bench.py's live key-switch VALU measurement (measurement
 infrastructure, not product): a few fhe_keyswitch_dist calls at the key-switch leg's shape (N = 2^16,
-L = 16, K = 4, dnum = 4, one-rank RCCL communicator, one chunk) on cuda:0, then the butterfly
+L = 16, K = 4, dnum = 4, one-rank RCCL communicator, the leg's chunks) on cuda:0, then the butterfly
 ceiling kernels of tools/microbench/bfly_peak.hip, so that one `rocprofv3 --pmc SQ_INSTS_VALU
 SQ_WAVES` pass over this process counts the VALU instructions of every key-switch kernel and of the
 ceiling kernel.  Prints one JSON line: the calls made and the ceiling kernels' own HIP-event times.
 bench.py runs it as a child process (never exec).
-usage: python tools/ks_valu_probe.py --log-n 16 --batch 32 [--calls 4]"""
+usage: python tools/ks_valu_probe.py --log-n 16 --batch 32 [--chunks 1] [--calls 4]"""
 import argparse
 import ctypes
 import json
@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--calls", type=int, default=4)
     a = ap.parse_args()
     L, K, dnum = 16, 4, 4
@@ -40,9 +41,9 @@ def main():
     d2 = rows(ctx.moduli, (a.batch,))
     eb, ea = rows(ctx.all_moduli, (dnum,)), rows(ctx.all_moduli, (dnum,))
     comm = RcclComm()
-    ws = ctx.workspace(fc.load().fhe_keyswitch_dist_workspace(ctx.handle, comm.handle, a.batch, 1))
+    ws = ctx.workspace(fc.load().fhe_keyswitch_dist_workspace(ctx.handle, comm.handle, a.batch, a.chunks))
     for _ in range(a.calls):
-        ctx.keyswitch_dist(comm, d2, eb, ea, chunks=1, workspace=ws)
+        ctx.keyswitch_dist(comm, d2, eb, ea, chunks=a.chunks, workspace=ws)
     torch.cuda.synchronize()
     lib = ctypes.CDLL(os.environ.get("FHE_PEAK_LIB") or
                       os.path.join(ROOT, "tools", "microbench", "libbflypeak.so"))
@@ -56,7 +57,8 @@ def main():
             raise RuntimeError("fhe_peak_bfly failed")
         ms["inverse" if inv else "forward"] = t.value
     comm.close()
-    print(json.dumps({"calls": a.calls, "batch": a.batch, "peak_ms_per_launch": ms}))
+    print(json.dumps({"calls": a.calls, "batch": a.batch, "chunks": a.chunks,
+                      "peak_ms_per_launch": ms}))
 
 
 if __name__ == "__main__":

@@ -4,7 +4,8 @@
 # pass of instruction-mix / LDS counters over tools/time_ntt.py.  Summarise with
 # tools/pmc_summary.py <out>/<tag>.
 # usage: tools/pmc_stall.sh <out> [lib.so ...]   (PMC_CMD overrides the profiled command, e.g.
-#        PMC_CMD="bench.py --workload keyswitch --steps 20 --warmup 5 --no-cpu-baseline")
+#        PMC_CMD="bench.py --workload keyswitch --steps 20 --warmup 5 --no-cpu-baseline --no-pmc";
+#        a profiled bench.py must get --no-pmc: its own live PMC passes would nest a rocprofv3)
 set -o pipefail
 cmd=${PMC_CMD:-tools/time_ntt.py 16 64}
 out=$1; shift

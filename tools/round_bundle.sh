@@ -25,7 +25,7 @@ else
     tag=$(echo $w | cut -d' ' -f1 | tr -d '-')
     timeout -k 10 300 python3 bench.py --workload $w > "$out/bench_$tag.json" 2> "$out/bench_$tag.err" || exit $?
   done
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/ks/stats" -o run --output-format csv -- python3 bench.py --workload keyswitch --no-cpu-baseline --no-dist-check > "$out/ks.json" 2> "$out/ks.err" || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/ks/stats" -o run --output-format csv -- python3 bench.py --workload keyswitch --no-cpu-baseline --no-dist-check --no-pmc > "$out/ks.json" 2> "$out/ks.err" || exit $?
   bash tools/kspmc.sh "$out/k" || exit $?
 fi
 echo "bundle $part done"
