@@ -346,6 +346,35 @@ def measure_keyswitch_valu_live(log_n, batch, chunks=1, timeout_s=150):
     return ks, ceil, None
 
 
+def measure_keyswitch_traffic_live(log_n, batch, chunks=1, timeout_s=150):
+    """HBM bytes of one key-switch call (every kernel it launches) at the leg's shape, measured in
+    this run: a --pmc FETCH_SIZE pass and a --pmc WRITE_SIZE pass (separate: the two do not fit
+    one pass) over tools/ks_valu_probe.py --no-peak, summed over the calls' dispatches and divided
+    by the calls; read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB (the gfx950 correction, as
+    measure_traffic_live).  Returns ({kernel: bytes per call}, total bytes per call, None) or
+    (None, None, reason)."""
+    short = lambda k: k.replace("void fhe::(anonymous namespace)::", "").replace(  # noqa: E731
+        "void fhe::", "").split("(")[0]
+    per, calls = {}, None
+    for counter, scale in (("FETCH_SIZE", 2048), ("WRITE_SIZE", 1024)):
+        rows, out, why = rocprof_pmc([counter], "ks_valu_probe.py",
+                                     ["--log-n", str(log_n), "--batch", str(batch),
+                                      "--chunks", str(chunks), "--no-peak"], timeout_s)
+        if rows is None:
+            return None, None, why
+        try:
+            calls = json.loads(out.strip().splitlines()[-1])["calls"]
+        except (ValueError, IndexError, KeyError):
+            return None, None, "ks_valu_probe printed no result line"
+        for k, c, v in rows:
+            if c == counter and "fhe::" in k and "bfly_peak" not in k:
+                per[short(k)] = per.get(short(k), 0.0) + v * scale
+    if not per or not calls:
+        return None, None, "no key-switch dispatches in the traffic passes"
+    per = {k: v / calls for k, v in per.items()}
+    return per, int(sum(per.values())), None
+
+
 def roofline(kernel, alg_bytes, ms, shape):
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     traffic, src = traffic_from_profile(kernel, shape)
@@ -353,6 +382,16 @@ def roofline(kernel, alg_bytes, ms, shape):
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": src, "kernel": kernel, "alg_bytes_per_launch": alg_bytes,
             "kernel_ms": round(ms, 4)}
+
+
+def transform_roofline(kavg, alg_bytes, shape):
+    """HBM roofline of whole NTTs (2 x 8 x N algorithmic bytes per transform)
+    against the summed mean time of every pass launch of one step (column + row, and both
+    directions when the step runs both): what the transform achieves, not one pass of it."""
+    ms = sum(kavg.values())
+    out = roofline(" + ".join(kavg) + " (whole transform)", alg_bytes, ms, shape)
+    out["passes"] = sorted(kavg)
+    return out
 
 
 _PEAKS = {}
@@ -513,6 +552,10 @@ def run_hommult(args, world, rank):
                 out["keyswitch_leg"]["roofline_valu"] = legs["ks"].valu_roofline()
             except Exception as e:  # noqa: BLE001 -- a measurement, never a reason to fail the line
                 out["keyswitch_leg"]["roofline_valu"] = {"valu_live_error": repr(e), "frac": None}
+            try:
+                legs["ks"].traffic(out["keyswitch_leg"])
+            except Exception as e:  # noqa: BLE001 -- as above
+                out["keyswitch_leg"]["roofline"]["traffic_live_error"] = repr(e)
     # after every timed leg: the sharded paths against each rank's single-device result
     if not args.no_dist_check:
         out["dist_check"] = guarded_leg(lambda: dist_check(world, rank, hm_ctx=ctx,
@@ -643,8 +686,12 @@ def run_ntt(args, world, rank):
            "config": {"workload": "forward+inverse NTT, single-limb transforms", "log_n": args.log_n,
                       "limbs": L, "polys_per_gpu": polys, "parallelism": f"rns-limb-shard x{world}"},
            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
-           # every NTT pass reads and writes each coefficient once
-           "roofline": roofline(dom, polys * shard.nlimbs * n * 16, kavg[dom], shape)}
+           # the whole transform: one NTT reads and writes each coefficient once (16 B per
+           # coefficient per direction), over the summed time of its column and row passes
+           "roofline": transform_roofline(kavg, 2 * polys * shard.nlimbs * n * 16, shape),
+           # each pass alone (every pass moves the data once more)
+           "roofline_passes": {k: roofline(k, polys * shard.nlimbs * n * 16, v, shape)
+                               for k, v in kavg.items()}}
     # butterflies of the dominant pass: row passes run the last log R2 stages, column passes the
     # first log R1
     pb = polys * shard.nlimbs * (row_bflies(args.log_n) if "row" in dom
@@ -738,7 +785,6 @@ def run_ntt_batch(args, world, rank):
     dt, kavg = timed(step, args, world, 4 * args.steps + 4)
     ntts = P * L * args.steps
     shape = {"log_n": log_n, "polys": mine, "nlimbs": L}
-    dom = max(kavg, key=kavg.get)
     per_pass = mine * L * n * 16
     out = {"metric": "NTTs/sec, 1024 x N=2^17 x 32 RNS limbs (forward, batched); achieved HBM GB/s vs peak",
            "value": round(ntts / dt, 1), "unit": "NTT/s",
@@ -749,7 +795,8 @@ def run_ntt_batch(args, world, rank):
            # whole transform: read + write every coefficient once (two passes move it twice)
            "ntt_alg_hbm_gbps_per_gpu": round(ntts / world / dt * n * 16 / 1e9, 1),
            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
-           "roofline": roofline(dom, per_pass, kavg[dom], shape)}
+           "roofline": transform_roofline(kavg, per_pass, shape),
+           "roofline_passes": {k: roofline(k, per_pass, v, shape) for k, v in kavg.items()}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_ntt(ctx.moduli[:8], log_n, args.cpu_seconds)
@@ -856,7 +903,30 @@ class KeyswitchLeg:
         self.step_s = dt / targs.steps
         if world == 1 and valu:
             res["roofline_valu"] = self.valu_roofline()
+            self.traffic(res)
         return res
+
+    def traffic(self, res):
+        """roofline.traffic of the key-switch line: the HBM bytes every kernel of one call moves,
+        from this run's FETCH_SIZE / WRITE_SIZE passes, per key-switch like `achieved`; null and
+        the reason when the passes are off (--no-pmc) or fail."""
+        rf = res["roofline"]
+        if not self.live_pmc:
+            rf["traffic_live_error"] = "--no-pmc"
+            return
+        per, total, why = measure_keyswitch_traffic_live(self.log_n, self.B, self.chunks)
+        if total is None:
+            rf["traffic_live_error"] = why
+            return
+        alg = rf["alg_bytes_per_launch"]
+        rf["traffic"] = total // self.B
+        rf["traffic_over_alg"] = round(total / self.B / alg, 3)
+        rf["traffic_per_call_by_kernel"] = {k: int(v) for k, v in sorted(per.items())}
+        rf["traffic_source"] = (
+            "measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes "
+            f"(separate) over tools/ks_valu_probe.py --no-peak (batch {self.B}, {self.chunks} "
+            "chunk(s)), every key-switch kernel's dispatches summed per call, per key-switch; "
+            "read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB (gfx950 correction)")
 
     def valu_roofline(self):
         step_s = self.step_s

@@ -244,3 +244,31 @@ def test_rocprof_pmc_skips_under_a_profiler(monkeypatch):
         live, why3 = bench.measure_traffic_live("k_hommult_row", [])
         assert live is None and why3 == why
     assert bench.profiled_parent({"LD_PRELOAD": "/usr/lib/libother.so", "PATH": "/bin"}) is None
+
+
+def test_keyswitch_traffic_live_sums_kernels(monkeypatch):
+    """The key-switch line's roofline.traffic: FETCH_SIZE and WRITE_SIZE passes (separate) over
+    ks_valu_probe.py --no-peak at the leg's batch and chunks; every fhe:: kernel's dispatches summed
+    per call, read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB; other kernels ignored."""
+    seen = []
+
+    def fake(counters, probe, args, timeout_s=150):
+        seen.append((counters, probe, args))
+        c = counters[0]
+        rows = [("void fhe::(anonymous namespace)::k_modup_col<16, 16, 4>(args)", c, 100.0),
+                ("void fhe::(anonymous namespace)::k_modup_col<16, 16, 4>(args)", c, 100.0),
+                ("void fhe::(anonymous namespace)::k_ks_row_inner<16, 16, 4, true>(x)", c, 50.0),
+                ("ncclDevKernel_AllGather(x)", c, 1e9), ("other", "SQ_WAVES", 5.0)]
+        return rows, '{"calls": 2, "batch": 32, "chunks": 1}\n', None
+
+    monkeypatch.setattr(bench, "rocprof_pmc", fake)
+    per, total, why = bench.measure_keyswitch_traffic_live(16, 32, 1)
+    assert why is None and [s[0] for s in seen] == [["FETCH_SIZE"], ["WRITE_SIZE"]]
+    assert all(s[1] == "ks_valu_probe.py" and "--no-peak" in s[2] and
+               s[2][s[2].index("--chunks") + 1] == "1" for s in seen)
+    # per call: modup 200 KiB fetched x 2 + 200 KiB written over 2 calls
+    assert per["k_modup_col<16, 16, 4>"] == (200 * 2048 + 200 * 1024) / 2
+    assert per["k_ks_row_inner<16, 16, 4, true>"] == (50 * 2048 + 50 * 1024) / 2
+    assert total == int(sum(per.values()))
+    monkeypatch.setattr(bench, "rocprof_pmc", lambda *a, **k: (None, None, "skipped: x"))
+    assert bench.measure_keyswitch_traffic_live(16, 32) == (None, None, "skipped: x")

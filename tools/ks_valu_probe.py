@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--calls", type=int, default=4)
+    ap.add_argument("--no-peak", action="store_true",
+                    help="skip the ceiling kernels (bench.py's HBM-traffic passes count only the "
+                         "key-switch)")
     a = ap.parse_args()
     L, K, dnum = 16, 4, 4
     n = 1 << a.log_n
@@ -45,6 +48,10 @@ def main():
     for _ in range(a.calls):
         ctx.keyswitch_dist(comm, d2, eb, ea, chunks=a.chunks, workspace=ws)
     torch.cuda.synchronize()
+    if a.no_peak:
+        comm.close()
+        print(json.dumps({"calls": a.calls, "batch": a.batch, "chunks": a.chunks}))
+        return
     lib = ctypes.CDLL(os.environ.get("FHE_PEAK_LIB") or
                       os.path.join(ROOT, "tools", "microbench", "libbflypeak.so"))
     lib.fhe_peak_bfly.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
