@@ -278,6 +278,10 @@ size_t fhe_keyswitch_workspace(const fhe_ctx* c, uint32_t nlimbs, uint32_t batch
   return c ? keyswitch_workspace_bytes(c, nlimbs, batch) : 0;
 }
 
+uint32_t fhe_keyswitch_pass_batch(const fhe_ctx* c, uint32_t batch) {
+  return c ? ks_pass_batch(c, batch) : 0;
+}
+
 int fhe_keyswitch_shard(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t* c_all,
                         const uint64_t* d2_own, const uint64_t* evk_b, const uint64_t* evk_a,
                         uint32_t limb0, uint32_t nlimbs, uint32_t batch, void* ws,

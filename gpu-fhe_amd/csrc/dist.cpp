@@ -306,10 +306,12 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
   // d2 are live at a time, so ModUp reads its sources from the Infinity Cache the gather just
   // wrote instead of from HBM (all INTTs first left every chunk but the last evicted once the
   // gathered batch outgrew the cache: DESIGN.md §8)
+  // The "ks_dist_intt" mark covers chunk 0's INTT (+ gather on the caller's stream) only: chunk
+  // k + 1's INTT is queued inside chunk k's key-switch, so its time counts in that chunk's marks.
   if ((rc = issue(0))) return rc;
+  prof_mark(s, "ks_dist_intt");
   for (u32 k = 0; k < p.chunks; ++k) {
     if (k + 1 < p.chunks && (rc = issue(k + 1))) return rc;
-    if (k == 0) prof_mark(s, "ks_dist_intt");
     if (own_stream) FHE_HIP_CHECK(hipStreamWaitEvent(s, comm->ev_gather[k], 0));
     if ((rc = dist_ks_chunk(ctx, p, k, ks0, ks1, d2_own, evk_b, evk_a, gather, kws, s)))
       return rc;

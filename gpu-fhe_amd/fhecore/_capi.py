@@ -44,6 +44,7 @@ SIGNATURES = {
     "fhe_hommult": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
     "fhe_baseconv": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _vp]),
     "fhe_keyswitch_workspace": (_sz, [_vp, _u32, _u32]),
+    "fhe_keyswitch_pass_batch": (_u32, [_vp, _u32]),
     "fhe_keyswitch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
     "fhe_keyswitch_shard": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp,
                                    _vp]),

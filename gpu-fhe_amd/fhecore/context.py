@@ -290,7 +290,8 @@ class Context:
         ks0, ks1 = _empty_like(d2), _empty_like(d2)
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
-            lib.fhe_keyswitch_workspace(self._ptr, self.L, batch))
+            lib.fhe_keyswitch_workspace(self._ptr, self.L,
+                                        lib.fhe_keyswitch_pass_batch(self._ptr, batch)))
         with torch.cuda.device(self.device):
             check(lib.fhe_keyswitch(self._ptr, _ptr(ks0), _ptr(ks1), _ptr(d2), _ptr(evk_b),
                                     _ptr(evk_a), batch, _ptr(ws), _stream(d2)), "fhe_keyswitch")
@@ -340,7 +341,7 @@ class Context:
         out = _empty_like(ct)
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
-            lib.fhe_rotate_workspace(self._ptr, batch))
+            lib.fhe_rotate_workspace(self._ptr, lib.fhe_keyswitch_pass_batch(self._ptr, batch)))
         with torch.cuda.device(self.device):
             check(lib.fhe_rotate(self._ptr, _ptr(out), _ptr(ct), galois_elt, _ptr(rot_b),
                                  _ptr(rot_a), batch, _ptr(ws), _stream(ct)), "fhe_rotate")
@@ -478,7 +479,7 @@ class Context:
             _check_out(out, a, shape, "mul_relin: out")
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
-            lib.fhe_mul_relin_workspace(self._ptr, batch))
+            lib.fhe_mul_relin_workspace(self._ptr, lib.fhe_keyswitch_pass_batch(self._ptr, batch)))
         with torch.cuda.device(self.device):
             check(lib.fhe_mul_relin(self._ptr, _ptr(out), _ptr(a), _ptr(b), _ptr(evk_b),
                                     _ptr(evk_a), batch, int(rescale), _ptr(ws), _stream(a)),

@@ -143,6 +143,12 @@ int fhe_baseconv(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t
  * d2 (the Infinity Cache), so the internal workspace is sized for one pass; a caller's workspace
  * of the documented *_workspace(ctx, ..., batch) bytes is always large enough. */
 size_t fhe_keyswitch_workspace(const fhe_ctx* ctx, uint32_t nlimbs, uint32_t batch);
+/* The pass size of fhe_keyswitch / fhe_rotate / fhe_mul_relin for `batch` ciphertexts:
+ * min(batch, the ciphertexts whose L limbs fit 256 MiB), at least 1 (0 for batch 0).  A workspace
+ * of fhe_keyswitch_workspace(ctx, L, pass) (fhe_rotate_workspace(ctx, pass),
+ * fhe_mul_relin_workspace(ctx, pass)) bytes is enough for any batch those calls split into passes
+ * of that size. */
+uint32_t fhe_keyswitch_pass_batch(const fhe_ctx* ctx, uint32_t batch);
 int fhe_keyswitch(const fhe_ctx* ctx, uint64_t* ks0, uint64_t* ks1, const uint64_t* d2,
                   const uint64_t* evk_b, const uint64_t* evk_a, uint32_t batch, void* workspace,
                   fhe_stream_t stream);
