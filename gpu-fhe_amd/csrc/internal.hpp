@@ -83,6 +83,18 @@ struct fhe_ctx {
   // the same with .y = D^_k 2^128 mod t: the fused lz16 ModUp's Montgomery conversion then emits
   // the extended rows times R = 2^64, so k_ks_row_inner's inner product reduces by one REDC
   ulonglong2* d_modup_hat_r = nullptr;  // [dnum][alpha][L + K]
+  // the fused conversions' tables (ntt.hip k_modup_col): {h, h w0 mod t} with h the .y word of
+  // d_modup_hat (_w), d_modup_hat_r (_rw), d_moddown_hat (_w) and w0 = psi_t^(N/2), the twiddle of
+  // the column-forward pass's stage 0, folded in for the rows that stage multiplies
+  ulonglong2* d_modup_hat_w = nullptr;    // [dnum][alpha][L + K]
+  ulonglong2* d_modup_hat_rw = nullptr;   // [dnum][alpha][L + K]
+  ulonglong2* d_moddown_hat_w = nullptr;  // [K][L + K]
+  // the same with P^-1 mod q folded into every Q-limb column (ModDown's P^-1 taken by the
+  // conversions and the accumulators instead of the finish: rns.hip pscale), and R P^-1 mod q_i
+  // for the own digit's d2 rows
+  ulonglong2* d_modup_hat_rwp = nullptr;   // [dnum][alpha][L + K]
+  ulonglong2* d_moddown_hat_wp = nullptr;  // [K][L + K]
+  ulonglong2* d_rpinv = nullptr;           // [L]
   ulonglong2* d_moddown_inv = nullptr;  // [K]                  (P^_k)^-1 mod p_k
   ulonglong2* d_moddown_hat = nullptr;  // [K][L + K]           P^_k mod q_i
   ulonglong2* d_pinv = nullptr;         // [L]                  P^-1 mod q_i
@@ -118,6 +130,12 @@ int launch_ntt(const fhe_ctx* c, bool forward, const u64* src, u64* dst, u32 pol
 int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstride, u64* dst,
                        u64 dpstride, u32 polys, u32 limb0, u32 nlimbs, hipStream_t s,
                        const ulonglong2* nfold = nullptr, bool split = false);
+// The second (column) pass of an inverse NTT alone, src [polys][nlimbs][N] (stride spstride,
+// already row-inverted, e.g. by k_ks_row_inner PINV) -> dst (stride dpstride); nfold / split as
+// launch_ntt_strided.
+int launch_ntt_col_inv(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
+                       u32 polys, u32 limb0, u32 nlimbs, hipStream_t s,
+                       const ulonglong2* nfold = nullptr, bool split = false);
 // Column-forward pass only (first half of a forward NTT; the key-switch's fused row kernel
 // finishes it).
 int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
@@ -139,6 +157,12 @@ struct KsRowArgs {
   // takes the own digit's d2 rows times R as well and reduces each 128-bit sum by one Montgomery
   // REDC (R^-1) instead of reduce128
   bool mont = false;
+  // the special rows leave row-inverted (the first pass of ModDown's INTT, k_ks_row_inner PINV):
+  // the caller follows with launch_ntt_col_inv only
+  u32 pinv = 0;
+  // per-limb Shoup pairs of the factor the own digit's d2 rows are taken times (MONT); null: R
+  // (ModParams::r64).  R P^-1 when ModDown's P^-1 is folded into the accumulators (rns.hip pscale)
+  const ulonglong2* rscale = nullptr;
 };
 int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s);
 // ModUp column pass (ntt.hip, k_modup_col): converts a digit's S pre-scaled source rows
@@ -151,7 +175,8 @@ struct ModUpColArgs {
   u64* ext;
   u64 rn;
   u32 S, T, skip_at, skip_len, n0, base0, base1, batch;
-  const ulonglong2* hat;  // this digit's conversion table: hat[k hs + limb]
+  // this digit's conversion table: hat[k hs + limb] = {h, h w0} (fhe_ctx::d_modup_hat_w)
+  const ulonglong2* hat;
   u32 hs;
 };
 int launch_modup_col(const fhe_ctx* c, const ModUpColArgs& a, hipStream_t s);
@@ -196,6 +221,9 @@ struct ModDownRowArgs {
   // 1: one set of polys (ks0 only, conv [batch][nq][N]), as the NTT-form rescale uses it
   u32 halves = 2;
   const ulonglong2* pinv = nullptr;  // per-limb Shoup pairs of the divisor's inverse; null: P^-1
+  // the accumulators' Q rows and conv already carry P^-1 (rns.hip pscale): the finish is
+  // acc - NTT(conv) mod q, no product
+  u32 prescaled = 0;
 };
 int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s);
 // NTT-form rescale, spread + column-forward pass in one (ntt.hip, k_rescale_col): last [polys][N]

@@ -296,8 +296,10 @@ constexpr int gs_in(int j, int k) {
 // per-lane twiddles from L2, whose latency then overlaps instead of stalling each stage).
 // ROWTAB: the twiddles come from a row table region (base = R1 + row), whose low-bit-round stages
 // are stored lane-major.
+// PRE0 (forward, k_modup_col): the operands of stage 0's products arrive already multiplied by
+// its twiddle (the base conversion folds it into its constants), so stage 0 only adds.
 template <int LOGR, int KB, int LO, bool FWD, int FIN, bool GATHER = false, int H = 8,
-          int RIN = 8, bool ROWTAB = GATHER, bool CHAIN = GATHER>
+          int RIN = 8, bool ROWTAB = GATHER, bool CHAIN = GATHER, bool PRE0 = false>
 __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
                                               const ulonglong2* __restrict__ tw, const u32 base,
                                               const u64 q, const ulonglong2 nf0,
@@ -367,8 +369,8 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
       constexpr int b = KB - 1 - done;
       constexpr int rin = fwd_range(RIN, done, H);
       constexpr bool reduce = rin + 3 > H;
-      const int bitpos = LO + b;
-      const int st = LOGR - 1 - bitpos;
+      constexpr int bitpos = LO + b;
+      constexpr int st = LOGR - 1 - bitpos;
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         if (j & (1 << b)) continue;
@@ -378,7 +380,13 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         if constexpr (reduce) u = H == 16 ? top_bits(u, sb, nq) : csubk(u, qh);
         FHE_OPAQUE(u);  // keeps 2u + 3q one v_lshl_add_u64 (not distributed over the select)
         // u + v straight out of the remainder chain; u - v + 3q = (2u + 3q) - (u + v)
-        u64 s = shoup_q3_add<CHAIN>(x[jj], w.x, w.y, nq, u);
+        u64 s;
+        if constexpr (PRE0 && st == 0) {
+          (void)w;
+          s = u + x[jj];  // x[jj] = w v below 2q: u + w v below (r + 2) q, u - w v + 3q below (r + 3) q
+        } else {
+          s = shoup_q3_add<CHAIN>(x[jj], w.x, w.y, nq, u);
+        }
         FHE_OPAQUE(s);
         x[j] = s;
         u64 t2 = (u << 1) + q3;
@@ -716,7 +724,7 @@ __device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
 // direct store instruction writes 16 of every 16 E bytes across 16 E * 64 bytes.
 // HALF: the column passes' one exchange (two rounds) through half the tile's LDS (half_exchange).
 template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, int H, int R0, bool XOUT = false,
-          bool CHAIN = GATHER, bool HALF = false, class GOut, class LV>
+          bool CHAIN = GATHER, bool HALF = false, bool PRE0 = false, class GOut, class LV>
 __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const LV& lv, u32 t,
                                          const ulonglong2* __restrict__ tw, u32 base, u64 q,
                                          ulonglong2 nf0, ulonglong2 nf1) {
@@ -739,7 +747,8 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     // column pass's few shared twiddles are left to the scheduler
     const ulonglong2* twk = tw;
     if constexpr (GATHER) asm volatile("" : "+s"(twk));
-    round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN, GATHER, CHAIN>(x, tp, twk, base, q, nf0, nf1);
+    round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN, GATHER, CHAIN, PRE0 && k == 0>(
+        x, tp, twk, base, q, nf0, nf1);
     if constexpr (k == Rd::NR - 1) {
       if constexpr (XOUT) {
         constexpr u32 TPS = (1u << LOGR) / kE;
@@ -1170,13 +1179,22 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   const u32 tp = Lay0::tpos(t);
   const gptr_u64 yb = (gptr_u64)(y + (u64)b * ybs + (u64)tile * G::SUBS_C + sub);
   u64 x[kE];
+  // Stage 0 of the column-forward pass multiplies the upper half of the rows (position bit
+  // N1 - 1) by its one twiddle w0 = psi^(N/2): the tables carry {h, h w0 mod t} pairs (rns.hip
+  // build_rns_tables), so those rows are converted straight into w0 x and stage 0 only adds
+  // (pass_run PRE0): 8 Shoup products per thread fewer.
+  auto upper = [](int j) { return ((Lay0::jpos(j) >> (G::N1 - 1)) & 1u) != 0; };
   if constexpr (H == 16) {
     // lz16 (every modulus < 2^60): plain sources, the S-term sum on 32-bit halves (dot_wide61:
     // no splitting, the low column's carries from the mads) and the subtractive REDC into (0, 2q)
     // (mont_redc: mont_redc_x's carry-mask asm does not survive this kernel's register allocation)
-    u64 hk[S];
+    u64 hk[S], hw[S];
 #pragma unroll
-    for (int k = 0; k < S; ++k) hk[k] = hat[(u64)k * hs + limb].y;
+    for (int k = 0; k < S; ++k) {
+      const ulonglong2 h = hat[(u64)k * hs + limb];
+      hk[k] = h.x;
+      hw[k] = h.y;
+    }
     const u64 qi = 0 - m.qinv;  // q^-1 mod 2^64
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
@@ -1185,28 +1203,32 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int k = 0; k < S; ++k) ys[k] = yb[dg.o[k] + i];
       u64 tlo, thi;
-      dot_wide61<S>(ys, hk, tlo, thi);
+      dot_wide61<S>(ys, upper(j) ? hw : hk, tlo, thi);
       x[j] = mont_redc(tlo, thi, m.q, qi);  // (0, 2q): the pass takes inputs below 2q
     }
   } else {
     // the constants' 30-bit pieces (Sum30: four v_mad_u64_u32 per term; sources arrive pre-split,
     // ks_split30)
-    u64 h2[S];
+    u64 h2[S], h2w[S];
 #pragma unroll
-    for (int k = 0; k < S; ++k) h2[k] = split30(hat[(u64)k * hs + limb].y);
+    for (int k = 0; k < S; ++k) {
+      const ulonglong2 h = hat[(u64)k * hs + limb];
+      h2[k] = split30(h.x);
+      h2w[k] = split30(h.y);
+    }
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
       const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
       Sum30 acc;
 #pragma unroll
-      for (int k = 0; k < S; ++k) acc.add(yb[dg.o[k] + i], h2[k]);
+      for (int k = 0; k < S; ++k) acc.add(yb[dg.o[k] + i], upper(j) ? h2w[k] : h2[k]);
       x[j] = acc.mont_lazy(m.q, m.qinv);  // [0, 2q): the pass takes inputs below 2q
     }
   }
   // mad-chain remainders (CHAIN) although this is a column pass: unlike the latency-bound column
   // passes of the NTTs, this one is VALU-bound (the conversion products): ModUp -1.1 %, ModDown
   // conversion pass -1 % same-box (profiles/r03_modup_chain_ab.txt)
-  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2, false, true, G::HALF_C>(
+  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2, false, true, G::HALF_C, true>(
       x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
       tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
 }
@@ -1226,6 +1248,11 @@ struct FinishView {
   u32 gal = 0;    // != 0: the addend is read through sigma_gal (hoisted rotation: sigma(c0))
   u32 rbase = 0;  // slot of add[0] within its poly
   u32 log_n = 0;
+  u32 pre = 0;    // != 0: acc and conv carry P^-1 already (ModDownRowArgs::prescaled)
+  __device__ __forceinline__ u64 fin(u64 a, u64 x) const {
+    if (pre) return csub(a + q - x, q);  // kernel-argument uniform
+    return csub(shoup_lazy(a + q - x, pinv.x, pinv.y, q), q);
+  }
   __device__ __forceinline__ u32 gal_src(u32 i) const {
     const u32 sh = 32 - log_n;
     const u32 g = ((2 * (__builtin_bitreverse32(i) >> sh) + 1) * gal) & ((2u << log_n) - 1);
@@ -1252,9 +1279,7 @@ struct FinishView {
 #pragma unroll
     for (int j = 0; j < kE / 2; ++j) {
       const u64x2_t av = a[j];
-      const u64 r0 = csub(shoup_lazy(av.x + q - x[2 * j], pinv.x, pinv.y, q), q);
-      const u64 r1 = csub(shoup_lazy(av.y + q - x[2 * j + 1], pinv.x, pinv.y, q), q);
-      o[j] = plus(u64x2_t{r0, r1}, off + 2 * j);
+      o[j] = plus(u64x2_t{fin(av.x, x[2 * j]), fin(av.y, x[2 * j + 1])}, off + 2 * j);
     }
   }
   struct Pre {
@@ -1269,14 +1294,13 @@ struct FinishView {
     return pre;
   }
   template <u32 TPS>
-  __device__ __forceinline__ void store_lin(const u64 (&x)[kE], u32 t, const Pre& pre) const {
+  __device__ __forceinline__ void store_lin(const u64 (&x)[kE], u32 t, const Pre& pa) const {
     const gptr_u128 o = (gptr_u128)(out + lane) + t;
 #pragma unroll
     for (int jj = 0; jj < kE / 2; ++jj) {
-      const u64x2_t av = pre.a[jj];
-      const u64 r0 = csub(shoup_lazy(av.x + q - x[2 * jj], pinv.x, pinv.y, q), q);
-      const u64 r1 = csub(shoup_lazy(av.y + q - x[2 * jj + 1], pinv.x, pinv.y, q), q);
-      o[jj * TPS] = plus(u64x2_t{r0, r1}, lane + 2 * (t + jj * TPS));
+      const u64x2_t av = pa.a[jj];
+      o[jj * TPS] = plus(u64x2_t{fin(av.x, x[2 * jj]), fin(av.y, x[2 * jj + 1])},
+                         lane + 2 * (t + jj * TPS));
     }
   }
 };
@@ -1285,7 +1309,7 @@ template <int LOGN, int H>
 __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __restrict__ ks0,
                                         u64* __restrict__ ks1, const u64* __restrict__ acc,
                                         u64 acc_ws, u32 rows, u32 nq, u32 limb0, u32 batch,
-                                        u32 items, u32 halves,
+                                        u32 items, u32 halves, u32 prescaled,
                                         const ulonglong2* __restrict__ pinv,
                                         const ulonglong2* __restrict__ tw_all,
                                         const ModParams* __restrict__ mods, KsEpilogue ep) {
@@ -1313,7 +1337,7 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   const FinishView fo{(h ? ks1 : ks0) + (u64)b * ep.out_bs + (u64)l * N + rloc,
                       acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc,
                       add ? add + (u64)b * ep.add_bs + (u64)l * N + rloc : nullptr, lane, q,
-                      pinv[limb], ep.add_gal, (u32)rloc, (u32)LOGN};
+                      pinv[limb], ep.add_gal, (u32)rloc, (u32)LOGN, prescaled};
   // column-passed by k_modup_col (inputs below 2q) or k_ntt_col (below q)
   pass_run<G::N2, true, kFinalFwd, kWaveSync, true, H, fwd_range(2, G::N1, H), true>(
       x, fo, lv, t, tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, q, {0, 0}, {0, 0});
@@ -1334,6 +1358,10 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
 // digit's d2 rows are taken times R here (by its otherwise idle wave), and each output is one
 // subtractive REDC of the 128-bit sum (R^-1 cancels the factor) plus one subtraction, instead of
 // reduce128's two Shoup products and three subtractions.
+// PINV != 0 (ModDown follows, rns.hip fused_down): the special rows (r >= nq) of both
+// accumulators take the first pass of ModDown's INTT here, the inverse row pass, while the
+// workgroup still holds whole rows; they are stored row-inverted, and only the column inverse is
+// left to launch (launch_ntt_col_inv): no separate row-pass launch and no HBM round trip for it.
 template <int LOGN, int HR, int DNUM, bool MONT = false>
 __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
                                          const u64* __restrict__ ext, u64 ext_ds,
@@ -1341,7 +1369,9 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
                                          const u64* __restrict__ evk_b,
                                          const u64* __restrict__ evk_a, u32 rows, u32 nq,
                                          u32 base0, u32 base1, u32 alpha, u32 L, u32 batch,
+                                         u32 pinv, const ulonglong2* __restrict__ rscale,
                                          const ulonglong2* __restrict__ twf,
+                                         const ulonglong2* __restrict__ twi,
                                          const ModParams* __restrict__ mods) {
   static_assert(DNUM >= 1 && DNUM <= 4, "one thread group per digit, four groups");
   using G = Geo<LOGN>;
@@ -1391,10 +1421,11 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
       gin.template load_lin<H::TPS>(v, t);
       if constexpr (MONT) {
         // v R mod q into [0, 2q) (Shoup by R mod q: [0, 3q), one subtraction): the inner
-        // product's operands must stay below 2^61
+        // product's operands must stay below 2^61.  (R P^-1 with rscale: ModDown's P^-1 folded)
         const u64 nq = 0 - q;
+        const ulonglong2 rs = rscale ? rscale[limb] : make_ulonglong2(m.r64, m.r64s);
 #pragma unroll
-        for (int j = 0; j < kE; ++j) v[j] = csubk(shoup_q3(v[j], m.r64, m.r64s, nq), q);
+        for (int j = 0; j < kE; ++j) v[j] = csubk(shoup_q3(v[j], rs.x, rs.y, nq), q);
       }
 #pragma unroll
       for (int jj = 0; jj < kE / 2; ++jj) {
@@ -1513,6 +1544,30 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
       o1[e + h] = reduce128((u64)s1[h], (u64)(s1[h] >> 64), m);
     }
   }
+  }
+  if (pinv && r >= nq) {  // workgroup-uniform
+    // o0 / o1 of row crow -> slots 0 / 1 of that row in linear order (every wave's combine reads
+    // are done first); then wave h runs the inverse row pass of accumulator h's 4 rows
+    static_assert(CW == 4 && H::ROWS * H::TPS == 64, "one row per wave in the combine");
+    const LView<1, true> s0{lds + crow * H::ROWW}, s1{lds + crow * H::ROWW + G::RS};
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < CW; ++e) {
+      s0.s[s0.idx(cpos + e)] = o0[e];
+      s1.s[s1.idx(cpos + e)] = o1[e];
+    }
+    __syncthreads();
+    const u32 h = threadIdx.x / 64;  // wave index (uniform)
+    if (h < 2) {
+      using Lay0 = Layout<G::N2, Rd::kb_inv(0), Rd::lo_inv(0)>;
+      const LView<1, true> lv{rowlds + h * G::RS};
+      u64 x[kE];
+      lv.template load<Lay0>(x, Lay0::tpos(t));
+      pass_run<G::N2, false, kNotFinal, kWaveSync, true, HR, fwd_range(1, G::N1, HR)>(
+          x, GView<1>{acc + h * acc_ws + (u64)b * rn + (u64)r * N + loc, 0}, lv, t,
+          twi + (u64)limb * N, base, q, {0, 0}, {0, 0});
+    }
+    return;
   }
   gptr_u128 a0 = (gptr_u128)(acc + (u64)b * rn + okey);
   gptr_u128 a1 = (gptr_u128)(acc + acc_ws + (u64)b * rn + okey);
@@ -1730,11 +1785,11 @@ int ks_row_inner_dispatch(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
     if (HD == 16 && a.mont)                                                                     \
       k_ks_row_inner<LOGN, HD, k, HD == 16><<<g, H::THR, 0, s>>>(                               \
           a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.base0, \
-          a.base1, a.alpha, a.L, a.batch, c->d_tw_fwd, c->d_mods);                             \
+          a.base1, a.alpha, a.L, a.batch, a.pinv, a.rscale, c->d_tw_fwd, c->d_tw_inv, c->d_mods);\
     else                                                                                        \
       k_ks_row_inner<LOGN, HD, k><<<g, H::THR, 0, s>>>(                                         \
           a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.base0, \
-          a.base1, a.alpha, a.L, a.batch, c->d_tw_fwd, c->d_mods);                             \
+          a.base1, a.alpha, a.L, a.batch, a.pinv, a.rscale, c->d_tw_fwd, c->d_tw_inv, c->d_mods);\
     break;
     D(1) D(2) D(3) D(4)
 #undef D
@@ -1856,7 +1911,7 @@ int moddown_row_dispatch(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t 
   if (int rc = check_grid(item_blocks(items), G::THR_R, 1, 1, "moddown_row")) return rc;
   k_moddown_row<LOGN, HD><<<dim3((u32)((items + 7) / 8 * 8)), G::THR_R, 0, s>>>(
       a.conv, a.ks0, a.ks1, a.acc, a.acc_ws, a.rows, a.nq, a.limb0, a.batch, (u32)items, a.halves,
-      a.pinv ? a.pinv : c->d_pinv, c->d_tw_fwd, c->d_mods, a.ep);
+      a.prescaled, a.pinv ? a.pinv : c->d_pinv, c->d_tw_fwd, c->d_mods, a.ep);
   return kOk;
 }
 }  // namespace
@@ -1918,6 +1973,61 @@ int launch_ntt_strided(const fhe_ctx* c, bool forward, const u64* src, u64 spstr
   }
   set_error("unsupported log_n");
   return kUnsupported;
+}
+
+namespace {
+template <int LOGN, int HD>
+int col_inv_dispatch(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
+                     u32 polys, u32 limb0, u32 nlimbs, hipStream_t s, const ulonglong2* nfold,
+                     bool split) {
+  using G = Geo<LOGN>;
+  const u64 ic = (u64)polys * nlimbs * G::TILES_C;
+  if (int rc = check_grid(item_blocks(ic), G::THR_C, 1, 1, "ntt_col_inv")) return rc;
+  const PolyMap pm{1, spstride, 0, dpstride, 0, 0};
+  const ulonglong2* nf = nfold ? nfold : c->d_nfold;
+  if constexpr (HD != 2) {
+    if (split) {
+      k_ntt_col<LOGN, false, inv_h(HD), false, false, kFinalInvS30>
+          <<<item_grid(ic), G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic,
+                                              c->d_tw_inv, nf, c->d_mods);
+      prof_mark(s, "ntt_col_inv");
+      return kOk;
+    }
+  } else if (split) {
+    set_error("split30 INTT outputs need every modulus < 2^61");
+    return kUnsupported;
+  }
+  k_ntt_col<LOGN, false, inv_h(HD)><<<item_grid(ic), G::THR_C, 0, s>>>(
+      src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_inv, nf, c->d_mods);
+  prof_mark(s, "ntt_col_inv");
+  return kOk;
+}
+}  // namespace
+
+int launch_ntt_col_inv(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
+                       u32 polys, u32 limb0, u32 nlimbs, hipStream_t s, const ulonglong2* nfold,
+                       bool split) {
+  if ((u64)polys * nlimbs == 0) return kOk;
+  int rc = kUnsupported;
+  switch (c->log_n) {
+#define X(n)                                                                                     \
+  case n:                                                                                        \
+    rc = c->wide   ? col_inv_dispatch<n, 2>(c, src, spstride, dst, dpstride, polys, limb0,      \
+                                            nlimbs, s, nfold, split)                            \
+         : c->lz16 ? col_inv_dispatch<n, 16>(c, src, spstride, dst, dpstride, polys, limb0,     \
+                                             nlimbs, s, nfold, split)                           \
+                   : col_inv_dispatch<n, 8>(c, src, spstride, dst, dpstride, polys, limb0,      \
+                                            nlimbs, s, nfold, split);                           \
+    break;
+    FHE_LOGN_CASES(X)
+#undef X
+    default:
+      set_error("unsupported log_n");
+      return kUnsupported;
+  }
+  if (rc) return rc;
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
 }
 
 size_t hommult_workspace_bytes(const fhe_ctx* c, u32 batch, u32 nlimbs) {

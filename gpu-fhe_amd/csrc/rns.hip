@@ -360,7 +360,33 @@ int build_rns_tables(fhe_ctx* c) {
     nf_down[4 * (L + k)] = shoup_pair(s, p);
     nf_down[4 * (L + k) + 1] = shoup_pair(mulmod_u64(w, s, p), p);
   }
+  // {h, h w0} for the fused conversions (k_modup_col folds stage 0's twiddle w0 = psi^(N/2) into
+  // the rows that stage multiplies)
+  // (pscale: times P^-1 mod t as well for the Q limbs t < L)
+  auto with_w0 = [&](const std::vector<Pair64>& hat, bool pscale) {
+    std::vector<Pair64> out(hat.size());
+    for (size_t i = 0; i < hat.size(); ++i) {
+      const u32 t = (u32)(i % M);
+      const u64 tm = c->moduli[t];
+      const u64 w0 = powmod_u64(c->psi[t], c->n / 2, tm);
+      const u64 h = pscale && t < L ? mulmod_u64(hat[i].y, pinv[t].x, tm) : hat[i].y;
+      out[i] = Pair64{h, mulmod_u64(h, w0, tm)};
+    }
+    return out;
+  };
+  std::vector<Pair64> rpinv(L);
+  for (u32 i = 0; i < L; ++i) {
+    const u64 q = c->moduli[i];
+    rpinv[i] = shoup_pair(mulmod_u64((u64)(((u128)1 << 64) % q), pinv[i].x, q), q);
+  }
   int rc;
+  if ((rc = upload(&c->d_modup_hat_w, with_w0(up_hat, false))) ||
+      (rc = upload(&c->d_modup_hat_rw, with_w0(up_hat_r, false))) ||
+      (rc = upload(&c->d_moddown_hat_w, with_w0(dn_hat, false))) ||
+      (rc = upload(&c->d_modup_hat_rwp, with_w0(up_hat_r, true))) ||
+      (rc = upload(&c->d_moddown_hat_wp, with_w0(dn_hat, true))) ||
+      (rc = upload(&c->d_rpinv, rpinv)))
+    return rc;
   if ((rc = upload(&c->d_modup_inv, up_inv)) || (rc = upload(&c->d_modup_hat, up_hat)) ||
       (rc = upload(&c->d_modup_hat_r, up_hat_r)) ||
       (rc = upload(&c->d_moddown_inv, dn_inv)) || (rc = upload(&c->d_moddown_hat, dn_hat)) ||
@@ -437,6 +463,10 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   // the unfused k_moddown_finish
   const bool fused_down = K <= 4 && ((fused && (u64)c->dnum * rows >= 2 * (u64)K) ||
                                      (hoist && hoist->ydn && ks_hoist_fused_down(c)));
+  // ModDown's P^-1 folded into the accumulators' Q rows (the ModUp conversion tables of the Q
+  // targets and the own digit's R factor carry P^-1) and into the P -> Q conversion table, so
+  // k_moddown_row's finish is a subtraction: the lz16 fused ModUp with the fused ModDown
+  const bool pscale = mont_ext && fused_down;
   // k_moddown_finish adds its addend rows un-permuted: a sigma-gathered addend
   // (KsEpilogue::add_gal, which only k_moddown_row implements) reaching it would give a wrong
   // ciphertext with no error, so a caller whose path predicate (ks_fused / ks_hoist_fused_down)
@@ -482,7 +512,10 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
       const u32 skip_at = skip_len ? own_lo - limb0 : rows;
       const ModUpColArgs ma{ysrc, ybs, {yoff[0], yoff[1], yoff[2], yoff[3]}, e, rn, S,
                             rows - skip_len, skip_at, skip_len, nlimbs, limb0, L, batch,
-                            (mont_ext ? c->d_modup_hat_r : c->d_modup_hat) + (size_t)j * alpha * M,
+                            (pscale     ? c->d_modup_hat_rwp
+                             : mont_ext ? c->d_modup_hat_rw
+                                        : c->d_modup_hat_w) +
+                                (size_t)j * alpha * M,
                             M};
       if (call.scaled && npend < 4) {
         pend[npend++] = ma;
@@ -506,9 +539,13 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   prof_mark(s, "ks_modup");
   if (hoist) return kOk;  // modup_only: the NTT-form digits stay in the workspace's ext region
   }
+  // the fused row kernel also runs the first (row) pass of ModDown's INTT on the special rows
+  const bool row_pinv = fused && fused_down;
   if (fused) {
-    const KsRowArgs ka{acc, acc_ws, ext, B * rn, d2_own, evk_b, evk_a, rows, nlimbs, limb0, L,
-                       alpha, L, batch, mont_ext};
+    KsRowArgs ka{acc, acc_ws, ext, B * rn, d2_own, evk_b, evk_a, rows, nlimbs, limb0, L,
+                 alpha, L, batch, mont_ext};
+    ka.pinv = row_pinv ? 1u : 0u;
+    ka.rscale = pscale ? c->d_rpinv : nullptr;
     if ((rc = launch_ks_row_inner(c, ka, s))) return rc;
   }
   const dim3 gi((u32)(n / kThreads), rows);
@@ -533,15 +570,19 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     // the INTT writes y = [x_k (P^_k)^-1]_{p_k} straight into [2 batch][K][N] (its last stage
     // folds N^-1 (P^_k)^-1, c->d_nfold_down): no separate scaling pass
     u64* ydn = hoist ? hoist->ydn : ext;
-    if ((rc = launch_ntt_strided(c, false, accp, rn, ydn, (u64)K * n, 2 * batch, L, K, s,
-                                 c->d_nfold_down, ks_split30(c))))
+    if ((rc = row_pinv ? launch_ntt_col_inv(c, accp, rn, ydn, (u64)K * n, 2 * batch, L, K, s,
+                                            c->d_nfold_down, ks_split30(c))
+                       : launch_ntt_strided(c, false, accp, rn, ydn, (u64)K * n, 2 * batch, L, K,
+                                            s, c->d_nfold_down, ks_split30(c))))
       return rc;
     prof_mark(s, "ks_moddown_conv");
     const ModUpColArgs md{ydn, (u64)K * n, {0, n, 2 * n, 3 * n}, conv, (u64)nlimbs * n, K, nlimbs,
-                          nlimbs, 0, nlimbs, limb0, 0, 2 * batch, c->d_moddown_hat, M};
+                          nlimbs, 0, nlimbs, limb0, 0, 2 * batch,
+                          pscale ? c->d_moddown_hat_wp : c->d_moddown_hat_w, M};
     if ((rc = launch_modup_col(c, md, s))) return rc;
     prof_mark(s, "ks_moddown_col");
-    const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch, ep};
+    ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch, ep};
+    da.prescaled = pscale ? 1u : 0u;
     if ((rc = launch_moddown_row(c, da, s))) return rc;
     prof_mark(s, "moddown_row_finish");
     return kOk;
