@@ -1137,6 +1137,11 @@ struct ModUpDigits {
 // hot in its L2.  Target tr -> row r = tr < skip_at ? tr : tr + skip_len (the digit's own rows are
 // skipped) -> limb r < n0 ? base0 + r : base1 + (r - n0).  Every digit of a ModUp runs in this
 // one launch (md.n digits with the same S, block ranges in digit order: no launch tail per digit).
+// Targets per workgroup: the S source tiles are loaded once and converted for kModupTG targets.
+// 1: two targets per workgroup (half the source loads) hold both converted tiles through the
+// first target's pass, 128 VGPRs with spills: ModUp 0.50 -> 0.60 ms (profiles/
+// r05_modup_targets_per_wg_ab.txt).
+constexpr u32 kModupTG = 1;
 template <int LOGN, int H, int S>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     4, 8))) void k_modup_col(const u64* __restrict__ y, u64 ybs, const ModUpDigits md, u64 rn,
@@ -1147,6 +1152,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
   using Rd = Rounds<G::N1>;
   using Lay0 = Layout<G::N1, Rd::kb(0), Rd::lo_fwd(0)>;
   constexpr u64 N = 1ull << LOGN;
+  constexpr u32 TG = kModupTG;
   __shared__ u64 lds[G::LDS_CF];
   const u32 sub = threadIdx.x % G::SUBS_C, t = threadIdx.x / G::SUBS_C;
   const LViewC<G::SUBS_C> lv{lds + sub};
@@ -1156,29 +1162,36 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     if (k < md.n && blockIdx.x >= md.d[k].blk0) di = k;
   const ModUpDigit& dg = md.d[di];
   const u32 T = dg.T, skip_at = dg.skip_at, skip_len = dg.skip_len;
+  const u32 TP = (T + TG - 1) / TG;  // target groups
   u64* __restrict__ ext = dg.ext;
   const ulonglong2* __restrict__ hat = dg.hat;
   const u32 blk = blockIdx.x - dg.blk0;
   const u32 nbt = batch * G::TILES_C;
-  u32 tr, bt;
+  u32 tg, bt;
   // (Tile-major per XCD instead, as k_ntt_col's placement -- a (target, ciphertext) pair's 16
   // tiles back to back on one XCD, the sources then read by every XCD: ModUp 0.252 -> 0.277 ms,
   // profiles/r03_row_order_ab.txt)
   if (nbt % 8 == 0) {  // every digit's block range then starts at a multiple of 8
     const u32 xcd = blk % 8, k8 = blk / 8;
-    tr = k8 % T;
-    bt = xcd + 8 * (k8 / T);
+    tg = k8 % TP;
+    bt = xcd + 8 * (k8 / TP);
   } else {
-    tr = blk % T;
-    bt = blk / T;
+    tg = blk % TP;
+    bt = blk / TP;
   }
   const u32 b = bt / G::TILES_C, tile = bt % G::TILES_C;
-  const u32 r = tr < skip_at ? tr : tr + skip_len;
-  const u32 limb = __builtin_amdgcn_readfirstlane(r < n0 ? base0 + r : base1 + (r - n0));
-  const ModParams m = mods[limb];
+  u32 rr[TG], limbs[TG];
+  bool live[TG];
+#pragma unroll
+  for (u32 g = 0; g < TG; ++g) {
+    const u32 tr = tg * TG + g;
+    live[g] = tr < T;
+    rr[g] = tr < skip_at ? tr : tr + skip_len;
+    limbs[g] = __builtin_amdgcn_readfirstlane(rr[g] < n0 ? base0 + rr[g] : base1 + (rr[g] - n0));
+  }
   const u32 tp = Lay0::tpos(t);
   const gptr_u64 yb = (gptr_u64)(y + (u64)b * ybs + (u64)tile * G::SUBS_C + sub);
-  u64 x[kE];
+  u64 x[TG][kE];
   // Stage 0 of the column-forward pass multiplies the upper half of the rows (position bit
   // N1 - 1) by its one twiddle w0 = psi^(N/2): the tables carry {h, h w0 mod t} pairs (rns.hip
   // build_rns_tables), so those rows are converted straight into w0 x and stage 0 only adds
@@ -1188,49 +1201,73 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(
     // lz16 (every modulus < 2^60): plain sources, the S-term sum on 32-bit halves (dot_wide61:
     // no splitting, the low column's carries from the mads) and the subtractive REDC into (0, 2q)
     // (mont_redc: mont_redc_x's carry-mask asm does not survive this kernel's register allocation)
-    u64 hk[S], hw[S];
+    u64 hk[TG][S], hw[TG][S], qq[TG], qi[TG];
 #pragma unroll
-    for (int k = 0; k < S; ++k) {
-      const ulonglong2 h = hat[(u64)k * hs + limb];
-      hk[k] = h.x;
-      hw[k] = h.y;
+    for (u32 g = 0; g < TG; ++g) {
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const ulonglong2 h = hat[(u64)k * hs + limbs[g]];
+        hk[g][k] = h.x;
+        hw[g][k] = h.y;
+      }
+      qq[g] = mods[limbs[g]].q;
+      qi[g] = 0 - mods[limbs[g]].qinv;  // q^-1 mod 2^64
     }
-    const u64 qi = 0 - m.qinv;  // q^-1 mod 2^64
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
       const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
       u64 ys[S];
 #pragma unroll
       for (int k = 0; k < S; ++k) ys[k] = yb[dg.o[k] + i];
-      u64 tlo, thi;
-      dot_wide61<S>(ys, upper(j) ? hw : hk, tlo, thi);
-      x[j] = mont_redc(tlo, thi, m.q, qi);  // (0, 2q): the pass takes inputs below 2q
+#pragma unroll
+      for (u32 g = 0; g < TG; ++g) {
+        u64 tlo, thi;
+        dot_wide61<S>(ys, upper(j) ? hw[g] : hk[g], tlo, thi);
+        x[g][j] = mont_redc(tlo, thi, qq[g], qi[g]);  // (0, 2q): the pass takes inputs below 2q
+      }
     }
   } else {
     // the constants' 30-bit pieces (Sum30: four v_mad_u64_u32 per term; sources arrive pre-split,
     // ks_split30)
-    u64 h2[S], h2w[S];
+    u64 h2[TG][S], h2w[TG][S];
 #pragma unroll
-    for (int k = 0; k < S; ++k) {
-      const ulonglong2 h = hat[(u64)k * hs + limb];
-      h2[k] = split30(h.x);
-      h2w[k] = split30(h.y);
+    for (u32 g = 0; g < TG; ++g) {
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const ulonglong2 h = hat[(u64)k * hs + limbs[g]];
+        h2[g][k] = split30(h.x);
+        h2w[g][k] = split30(h.y);
+      }
     }
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
       const u64 i = (u64)(tp | Lay0::jpos(j)) * G::R2;
-      Sum30 acc;
+      u64 ys[S];
 #pragma unroll
-      for (int k = 0; k < S; ++k) acc.add(yb[dg.o[k] + i], upper(j) ? h2w[k] : h2[k]);
-      x[j] = acc.mont_lazy(m.q, m.qinv);  // [0, 2q): the pass takes inputs below 2q
+      for (int k = 0; k < S; ++k) ys[k] = yb[dg.o[k] + i];
+#pragma unroll
+      for (u32 g = 0; g < TG; ++g) {
+        Sum30 acc;
+#pragma unroll
+        for (int k = 0; k < S; ++k) acc.add(ys[k], upper(j) ? h2w[g][k] : h2[g][k]);
+        const ModParams& mg = mods[limbs[g]];
+        x[g][j] = acc.mont_lazy(mg.q, mg.qinv);  // [0, 2q): the pass takes inputs below 2q
+      }
     }
   }
   // mad-chain remainders (CHAIN) although this is a column pass: unlike the latency-bound column
   // passes of the NTTs, this one is VALU-bound (the conversion products): ModUp -1.1 %, ModDown
   // conversion pass -1 % same-box (profiles/r03_modup_chain_ab.txt)
-  pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2, false, true, G::HALF_C, true>(
-      x, GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)r * N + (u64)tile * G::SUBS_C, sub}, lv, t,
-      tw_all + (u64)limb * N, 1u, m.q, {0, 0}, {0, 0});
+  static_for<0, (int)TG>([&](auto gc) {
+    constexpr int g = decltype(gc)::value;
+    if (!live[g]) return;  // workgroup-uniform
+    if (g > 0) __syncthreads();  // the previous target's exchange reads are done
+    const u32 lg = __builtin_amdgcn_readfirstlane(limbs[g]);
+    const u32 rg = __builtin_amdgcn_readfirstlane(rr[g]);
+    pass_run<G::N1, true, kNotFinal, kBlockSync, false, H, 2, false, true, G::HALF_C, true>(
+        x[g], GView<G::R2, false, kKsNT>{ext + (u64)b * rn + (u64)rg * N + (u64)tile * G::SUBS_C, sub},
+        lv, t, tw_all + (u64)lg * N, 1u, mods[lg].q, {0, 0}, {0, 0});
+  });
 }
 
 // ModDown's last step fused into the row-forward pass of the conversion NTT (key-switch):
@@ -1840,7 +1877,7 @@ int modup_col_dispatch(const fhe_ctx* c, const ModUpColArgs* a, u32 n, hipStream
     d.skip_at = a[k].skip_at;
     d.skip_len = a[k].skip_len;
     d.blk0 = (u32)blocks;
-    blocks += (u64)a[k].T * a[k].batch * G::TILES_C;
+    blocks += (u64)((a[k].T + kModupTG - 1) / kModupTG) * a[k].batch * G::TILES_C;
     if (int rc = check_grid(blocks, G::THR_C, 1, 1, "modup_col")) return rc;
   }
   const ModUpColArgs& a0 = a[0];

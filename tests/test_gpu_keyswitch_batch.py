@@ -55,3 +55,31 @@ def test_batched_shards_concatenate(ks_setup, G):
     g0, g1 = np.concatenate(parts0, axis=1), np.concatenate(parts1, axis=1)
     for i, (r0, r1) in enumerate(ref):
         assert (g0[i] == r0).all() and (g1[i] == r1).all()
+
+
+def test_pass_batch_and_pass_sized_workspaces(ks_setup):
+    """fhe_keyswitch_pass_batch: the pass size the single-device key-switch, rotate and mul-relin
+    split a batch into (256 MiB of L limbs: 32 ciphertexts at N = 2^16, L = 16), and the Python
+    wrappers size their workspaces for one pass, not for the whole batch."""
+    fc, ctx, d2, eb, ea, ref = ks_setup
+    lib = fc.load()
+    p = lambda b: lib.fhe_keyswitch_pass_batch(ctx.handle, b)  # noqa: E731
+    assert (p(0), p(1), p(31), p(32), p(33), p(1000)) == (0, 1, 31, 32, 32, 32)
+    sized = []
+    orig = ctx.workspace
+
+    def spy(nbytes):
+        sized.append(nbytes)
+        return orig(nbytes)
+
+    ctx.workspace = spy
+    try:
+        big = np.concatenate([d2] * 11 + [d2[:1]])  # 34 ciphertexts: two passes
+        k0, k1 = ctx.keyswitch(fc.to_device(big), fc.to_device(eb), fc.to_device(ea))
+    finally:
+        del ctx.workspace
+    assert sized == [lib.fhe_keyswitch_workspace(ctx.handle, ctx.L, 32)]
+    k0, k1 = fc.to_host(k0), fc.to_host(k1)
+    for i in range(big.shape[0]):
+        r0, r1 = ref[i % d2.shape[0]]
+        assert (k0[i] == r0).all() and (k1[i] == r1).all(), i
