@@ -1,0 +1,5 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r5f2
+bash tools/round_bundle.sh gpurun_out/r5f2 A || exit $?
+bash tools/round_bundle.sh gpurun_out/r5f2 B || exit $?
+echo final bundle done
