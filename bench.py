@@ -311,6 +311,54 @@ def measure_traffic_live(kernel_match, probe_args, timeout_s=150):
     return int(2 * 1024 * per["FETCH_SIZE"] + 1024 * per["WRITE_SIZE"]), None
 
 
+def measure_hommult_valu_live(log_n, limbs, batch, kernel_ms, timeout_s=150):
+    """VALU issue of k_hommult_row measured in this run: one `rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES
+    GRBM_GUI_ACTIVE` pass over tools/hm_traffic_probe.py --peak (the HomMult at the bench shape, then
+    the butterfly ceiling kernels in the same process).  VALU instructions per launch over this
+    run's HIP-event time give the achieved rate; the ceiling is the faster of the two ceiling
+    kernels; GRBM_GUI_ACTIVE per dispatch / 8 XCDs / duration gives each kernel's clock, so
+    `frac_per_cycle` = frac x ceiling clock / kernel clock separates issue efficiency from clock.
+    Returns (dict, None) or (None, reason)."""
+    rows, out, why = rocprof_pmc(["SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE"],
+                                 "hm_traffic_probe.py",
+                                 ["--log-n", str(log_n), "--limbs", str(limbs), "--batch",
+                                  str(batch), "--peak"], timeout_s)
+    if rows is None:
+        return None, why
+    try:
+        meta = json.loads(out.strip().splitlines()[-1])
+        peak_ms = meta["peak_ms_per_launch"]
+    except (ValueError, IndexError, KeyError):
+        return None, "hm_traffic_probe printed no result line"
+    per = {}
+    for k, c, v in rows:
+        key = ("hm" if "k_hommult_row" in k else "inverse" if "k_bfly_peak<true>" in k
+               else "forward" if "k_bfly_peak<false>" in k else None)
+        if key:
+            per.setdefault(key, {}).setdefault(c, []).append(v)
+    mean = lambda key, c: sum(per[key][c]) / len(per[key][c])  # noqa: E731
+    try:
+        hm_valu, hm_grbm = mean("hm", "SQ_INSTS_VALU"), mean("hm", "GRBM_GUI_ACTIVE")
+        ceil = {k: (mean(k, "SQ_INSTS_VALU") / (peak_ms[k] * 1e-3) / 1e9,
+                    mean(k, "GRBM_GUI_ACTIVE") / 8 / (peak_ms[k] * 1e-3) / 1e9)
+                for k in ("forward", "inverse")}
+    except (KeyError, ZeroDivisionError):
+        return None, "no k_hommult_row or ceiling dispatches in the VALU pass"
+    ceil_rate, ceil_clock = max(ceil.values())
+    achieved = hm_valu / (kernel_ms * 1e-3) / 1e9
+    clock = hm_grbm / 8 / (kernel_ms * 1e-3) / 1e9
+    frac = achieved / ceil_rate
+    return {"bound": "valu", "achieved": round(achieved, 1), "peak": round(ceil_rate, 1),
+            "unit": "G VALU wave-instructions/s", "frac": round(frac, 4),
+            "kernel": "hm_row_tensor (k_hommult_row)", "valu_instr_per_launch": round(hm_valu),
+            "clock_ghz": round(clock, 3), "peak_clock_ghz": round(ceil_clock, 3),
+            "frac_per_cycle": round(frac * ceil_clock / clock, 4) if clock else None,
+            "valu_source": "measured in this run: rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES "
+                           "GRBM_GUI_ACTIVE over tools/hm_traffic_probe.py --peak (same shape; "
+                           "ceiling = k_bfly_peak in that process); time from this run's HIP "
+                           "events"}, None
+
+
 def measure_keyswitch_valu_live(log_n, batch, chunks=1, timeout_s=150):
     """SQ_INSTS_VALU of one key-switch call at the leg's shape and chunking, measured in this run: one
     `rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES` pass over tools/ks_valu_probe.py, which makes a few
@@ -538,6 +586,9 @@ def run_hommult(args, world, rank):
             rf["traffic_over_alg_with_twiddles"] = round(live / (alg + tw), 4)
         else:
             rf["traffic_live_error"] = why
+        valu, why = measure_hommult_valu_live(args.log_n, L, gbatch, rf["kernel_ms"])
+        out["roofline_valu"] = valu if valu is not None else {"valu_live_error": why,
+                                                               "frac": None}
     legs = {}
     if not (args.no_keyswitch_leg or args.bits != 60):
         def ks_leg():

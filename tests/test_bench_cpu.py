@@ -272,3 +272,31 @@ def test_keyswitch_traffic_live_sums_kernels(monkeypatch):
     assert total == int(sum(per.values()))
     monkeypatch.setattr(bench, "rocprof_pmc", lambda *a, **k: (None, None, "skipped: x"))
     assert bench.measure_keyswitch_traffic_live(16, 32) == (None, None, "skipped: x")
+
+
+def test_hommult_valu_live_rates_and_clocks(monkeypatch):
+    """The HomMult line's roofline_valu: one SQ_INSTS_VALU / SQ_WAVES / GRBM_GUI_ACTIVE pass over
+    hm_traffic_probe.py --peak; achieved = VALU per k_hommult_row launch over the run's kernel
+    time, ceiling = the faster k_bfly_peak, clocks from GRBM_GUI_ACTIVE / 8 XCDs / duration."""
+    seen = {}
+
+    def fake(counters, probe, args, timeout_s=150):
+        seen.update(counters=counters, probe=probe, args=args)
+        rows = []
+        for k, valu, grbm in (("void fhe::(anonymous namespace)::k_hommult_row<16, 16>(x)", 4e8, 8 * 2e6),
+                              ("void (anonymous namespace)::k_bfly_peak<false>(x)", 6e8, 8 * 2.4e6),
+                              ("void (anonymous namespace)::k_bfly_peak<true>(x)", 5e8, 8 * 2.4e6)):
+            rows += [(k, "SQ_INSTS_VALU", valu), (k, "GRBM_GUI_ACTIVE", grbm), (k, "SQ_WAVES", 1.0)]
+        meta = '{"calls": 4, "batch": 64, "peak_ms_per_launch": {"forward": 1.0, "inverse": 1.0}}\n'
+        return rows, meta, None
+
+    monkeypatch.setattr(bench, "rocprof_pmc", fake)
+    r, why = bench.measure_hommult_valu_live(16, 8, 64, 1.0)
+    assert why is None and seen["probe"] == "hm_traffic_probe.py" and "--peak" in seen["args"]
+    assert seen["counters"] == ["SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE"]
+    assert r["achieved"] == pytest.approx(400.0) and r["peak"] == pytest.approx(600.0)
+    assert r["frac"] == pytest.approx(400 / 600, abs=1e-4)
+    assert r["clock_ghz"] == pytest.approx(2.0) and r["peak_clock_ghz"] == pytest.approx(2.4)
+    assert r["frac_per_cycle"] == pytest.approx(400 / 600 * 2.4 / 2.0, abs=1e-3)
+    monkeypatch.setattr(bench, "rocprof_pmc", lambda *a, **k: (None, None, "skipped: x"))
+    assert bench.measure_hommult_valu_live(16, 8, 64, 1.0) == (None, "skipped: x")

@@ -366,6 +366,25 @@ def test_keyswitch_paths_match_oracle(fc, L, K, dnum, batch):
         assert (h0[b] == r0).all() and (h1[b] == r1).all(), b
 
 
+@pytest.mark.parametrize("log_n", [10, 11, 13, 14, 15, 17])
+def test_keyswitch_every_ring_degree(fc, log_n):
+    """The fused key-switch (row kernel with the inner product and ModDown's INTT row pass, the
+    stage-0-folded conversions, P^-1 in the constants) at every other supported N: the row-kernel
+    geometries differ (32 rows per workgroup at N = 2^10, too few tiles for the XCD placement
+    below 2^14, a row group spanning two wavefronts at 2^17)."""
+    L, K, dnum, batch = 4, 2, 2, 2
+    ctx = ctx_for(fc, log_n, L, K=K, dnum=dnum)
+    allm = ctx.all_moduli
+    d2 = rand(ctx.moduli, log_n, (batch,), seed=80 + log_n)
+    eb = rand(allm, log_n, (dnum,), seed=81)
+    ea = rand(allm, log_n, (dnum,), seed=82)
+    ks0, ks1 = ctx.keyswitch(fc.to_device(d2), fc.to_device(eb), fc.to_device(ea))
+    h0, h1 = fc.to_host(ks0), fc.to_host(ks1)
+    for b in range(batch):
+        r0, r1 = coracle.keyswitch(d2[b], eb, ea, ctx.moduli, ctx.special, dnum)
+        assert (h0[b] == r0).all() and (h1[b] == r1).all(), b
+
+
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_keyswitch_sharded_equals_unsharded(fc, G):
     """the G-way limb-sharded key-switch (one all-gather of INTT(d2)) concatenates to
