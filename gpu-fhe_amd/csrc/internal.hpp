@@ -163,6 +163,8 @@ struct KsRowArgs {
   // per-limb Shoup pairs of the factor the own digit's d2 rows are taken times (MONT); null: R
   // (ModParams::r64).  R P^-1 when ModDown's P^-1 is folded into the accumulators (rns.hip pscale)
   const ulonglong2* rscale = nullptr;
+  // the rows this launch covers: [row0, row0 + nrows) (nrows 0: all rows)
+  u32 row0 = 0, nrows = 0;
 };
 int launch_ks_row_inner(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s);
 // ModUp column pass (ntt.hip, k_modup_col): converts a digit's S pre-scaled source rows
@@ -197,6 +199,22 @@ struct KsEpilogue {
   u64 add_bs = 0;
   u32 add_gal = 0;  // != 0: add rows read through sigma_add_gal's NTT-domain gather (k_moddown_row)
 };
+// The Q rows with ModDown's finish (ntt.hip k_ks_row_fin; lz16 with P^-1 folded, after the P rows,
+// their column inverse and ModDown's conversion): ks{0,1} [batch][nq][N] (+ the epilogue)
+struct KsFinArgs {
+  const u64* ext;
+  u64 ext_ds;
+  const u64* d2_own;
+  const u64* evk_b;
+  const u64* evk_a;
+  u32 rows, nq, base0, alpha, L, batch;
+  const ulonglong2* rscale;  // R P^-1 per limb
+  const u64* conv;           // [2][batch][nq][N], column-passed
+  u64* ks0;
+  u64* ks1;
+  KsEpilogue ep;  // out_bs resolved
+};
+int launch_ks_row_fin(const fhe_ctx* c, const KsFinArgs& a, hipStream_t s);
 // Hoisted rotations (galois.hip launch_rotate_hoisted): modup_only runs ModUp alone and leaves the
 // NTT-form digits in the workspace's ext region; otherwise the key-switch skips ModUp and reads
 // those digits (and d2_own) through sigma_galois inside the inner product (unfused kernels).

@@ -1405,6 +1405,7 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
                                          const u64* __restrict__ d2_own,
                                          const u64* __restrict__ evk_b,
                                          const u64* __restrict__ evk_a, u32 rows, u32 nq,
+                                         u32 row0, u32 nrows,
                                          u32 base0, u32 base1, u32 alpha, u32 L, u32 batch,
                                          u32 pinv, const ulonglong2* __restrict__ rscale,
                                          const ulonglong2* __restrict__ twf,
@@ -1428,11 +1429,11 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
     tile = xcd + 8 * (k8 % T8);
     const u32 rb = k8 / T8;
     b = rb % batch;
-    r = rb / batch;
+    r = row0 + rb / batch;
   } else {  // small N: too few tiles to deal out by XCD
-    r = blockIdx.x % rows;
-    b = (blockIdx.x / rows) % batch;
-    tile = blockIdx.x / (rows * batch);
+    r = row0 + blockIdx.x % nrows;
+    b = (blockIdx.x / nrows) % batch;
+    tile = blockIdx.x / (nrows * batch);
   }
   const u32 limb = r < nq ? base0 + r : base1 + (r - nq);
   const ModParams m = mods[limb];
@@ -1613,6 +1614,183 @@ __global__ FHE_KATTR void k_ks_row_inner(u64* __restrict__ acc, u64 acc_ws,
     a0[e / 2] = u64x2_t{o0[e], o0[e + 1]};
     a1[e / 2] = u64x2_t{o1[e], o1[e + 1]};
   }
+}
+
+// The key-switch's Q rows with ModDown's finish in the same workgroup (lz16 contexts with P^-1
+// folded into the constants, rns.hip pscale): launched after the special rows (k_ks_row_inner
+// with PINV over rows [nq, rows)) and ModDown's conversion (k_modup_col: conv [2][batch][nq][N],
+// column-passed), so NTT(conv) can be taken here instead of in k_moddown_row, and the
+// accumulators' Q rows never go to HBM:
+//   * the own digit's wave, which had only d2 to load, runs conv_0's row-forward pass into its LDS
+//     slot; the combine reads the own digit's d2 words straight from global memory (times R P^-1);
+//   * out_0 = acc_0 - NTT(conv_0) mod q (+ the epilogue's addend) is stored at once, acc_1 stays in
+//     registers while one wave (an idle one when DNUM < 4, else wave 0 after a barrier) runs
+//     conv_1's row-forward pass, then out_1.
+// Same placement and thread groups as k_ks_row_inner; gridDim.x = nq * TILES * batch.
+template <int LOGN, int DNUM>
+__global__ FHE_KATTR void k_ks_row_fin(const u64* __restrict__ ext, u64 ext_ds,
+                                       const u64* __restrict__ d2_own,
+                                       const u64* __restrict__ evk_b,
+                                       const u64* __restrict__ evk_a, u32 rows, u32 nq,
+                                       u32 base0, u32 alpha, u32 L, u32 batch,
+                                       const ulonglong2* __restrict__ rscale,
+                                       const u64* __restrict__ conv, u64* __restrict__ ks0,
+                                       u64* __restrict__ ks1, KsEpilogue ep,
+                                       const ulonglong2* __restrict__ twf,
+                                       const ModParams* __restrict__ mods) {
+  static_assert(DNUM >= 1 && DNUM <= 4, "one thread group per digit, four groups");
+  constexpr int HR = 16;
+  using G = Geo<LOGN>;
+  using H = HmGeo<LOGN>;
+  using Rd = Rounds<G::N2>;
+  constexpr u64 N = 1ull << LOGN;
+  __shared__ u64 lds[H::ROWS * H::ROWW];
+  u32 b, r, tile;
+  if (H::TILES % 8 == 0) {
+    const u32 xcd = blockIdx.x % 8, k8 = blockIdx.x / 8;
+    constexpr u32 T8 = H::TILES / 8;
+    tile = xcd + 8 * (k8 % T8);
+    const u32 rb = k8 / T8;
+    b = rb % batch;
+    r = rb / batch;
+  } else {
+    r = blockIdx.x % nq;
+    b = (blockIdx.x / nq) % batch;
+    tile = blockIdx.x / (nq * batch);
+  }
+  const u32 limb = base0 + r;  // a Q row: its limb is this rank's own
+  const ModParams m = mods[limb];
+  const u64 q = m.q;
+  const u64 rn = (u64)rows * N;
+  const u32 grp = __builtin_amdgcn_readfirstlane(threadIdx.x / (H::ROWS * H::TPS));
+  const u32 sub = (threadIdx.x / H::TPS) % H::ROWS, t = threadIdx.x % H::TPS;
+  const u32 row = tile * H::ROWS + sub;
+  const u64 loc = (u64)row * G::R2;
+  const u32 base = (u32)G::R1 + row;
+  u64* rowlds = lds + sub * H::ROWW;
+  constexpr int SY = H::SYNC_ROUND;
+  using LayT = Layout<G::N2, Rd::kb(Rd::NR - 1), Rd::lo_fwd(Rd::NR - 1)>;
+  const u32 tpT = LayT::tpos(t);
+  const u32 od = __builtin_amdgcn_readfirstlane(limb / alpha);  // the own digit (< DNUM)
+  const ulonglong2* tf = twf + (u64)limb * N;
+  // row-forward pass of a column-passed row (inputs below 2q) into LDS slot `slot`; FIN: the last
+  // round's reduction (canonical for conv, [0, 2q) for the inner product's operands)
+  auto row_fwd = [&](const u64* src, u32 slot, auto fin) {
+    constexpr int FINAL = decltype(fin)::value;
+    const LView<1, true> sl{rowlds + slot * G::RS};
+    u64 v[kE];
+    static_for<0, Rd::NR>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int KB = Rd::kb(k);
+      constexpr int LO = Rd::lo_fwd(k);
+      constexpr int RIN = fwd_range(fwd_range(2, G::N1, HR), G::N2 - (LO + KB), HR);
+      using Lay = Layout<G::N2, KB, LO>;
+      const u32 tp = Lay::tpos(t);
+      if constexpr (k == 0) {
+        const GView<1, kKsNT> gin{const_cast<u64*>(src) + loc, 0};
+        gin.template load<Lay>(v, tp);
+      } else {
+        lds_sync<SY>();
+        sl.template load<Lay>(v, tp);
+      }
+      constexpr int F = k == Rd::NR - 1 ? FINAL : kNotFinal;
+      round_compute<G::N2, KB, LO, true, F, true, HR, RIN>(v, tp, tf, base, q, {0, 0}, {0, 0});
+      if constexpr (k < Rd::NR - 1) {
+        if (k > 0) lds_sync<SY>();
+        sl.template store<Lay>(v, tp);
+      }
+    });
+    lds_sync<SY>();
+    sl.template store<LayT>(v, tpT);
+  };
+  using FinC = std::integral_constant<int, kFinalFwd>;
+  using FinX = std::integral_constant<int, kFinalFwd2>;
+  const u64* conv0 = conv + ((u64)b * nq + r) * N;
+  const u64* conv1 = conv + ((u64)(batch + b) * nq + r) * N;
+  if (grp < (u32)DNUM) {
+    if (grp == od) row_fwd(conv0, grp, FinC{});
+    else row_fwd(ext + (u64)grp * ext_ds + (u64)b * rn + (u64)r * N, grp, FinX{});
+  } else if (grp == (u32)DNUM) {
+    row_fwd(conv1, grp, FinC{});  // an idle wave (DNUM < 4) takes conv_1 now
+  }
+  // combine operands: keys and the own digit's d2 words, issued before the barrier
+  constexpr int CW = (H::ROWS * G::R2) / H::THR;
+  static_assert(CW == 4 && H::ROWS * H::TPS == 64, "one row per wave in the combine");
+  const u32 cpos0 = threadIdx.x * CW;
+  const u32 crow = cpos0 / G::R2, cpos = cpos0 % G::R2;
+  const u64 orow = (u64)(tile * H::ROWS + crow) * G::R2 + cpos;  // position within the poly
+  const u64 okey = (u64)r * N + orow;
+  const u64* lrow = lds + crow * H::ROWW;
+  u64x2_t kbv[CW / 2][DNUM], kav[CW / 2][DNUM], dv[CW / 2];
+#pragma unroll
+  for (int e = 0; e < CW; e += 2) {
+#pragma unroll
+    for (int d = 0; d < DNUM; ++d) {
+      kbv[e / 2][d] = *(const __attribute__((address_space(1))) u64x2_t*)(evk_b + (u64)d * rn + okey + e);
+      kav[e / 2][d] = *(const __attribute__((address_space(1))) u64x2_t*)(evk_a + (u64)d * rn + okey + e);
+    }
+    dv[e / 2] = *(const __attribute__((address_space(1))) u64x2_t*)(d2_own + ((u64)b * nq + r) * N + orow + e);
+  }
+  __syncthreads();
+  u64 qi = 0 - m.qinv;  // q^-1 mod 2^64
+  asm("" : "+s"(qi));
+  const ulonglong2 rs = rscale[limb];  // R P^-1 mod q
+  const u64 nqm = 0 - q;
+  auto at = [&](u32 slot, u32 p) { return lrow[slot * G::RS + p + (p >> 4)]; };
+  u64 o1[CW], f0[CW];
+#pragma unroll
+  for (int e = 0; e < CW; e += 2) {
+    u64 x0[DNUM], x1[DNUM], kb0[DNUM], kb1[DNUM], ka0[DNUM], ka1[DNUM];
+    // the own digit's slot holds NTT(conv_0): its operand is d2 R P^-1 instead, in [0, 2q)
+    const u64 xo0 = csubk(shoup_q3(dv[e / 2].x, rs.x, rs.y, nqm), q);
+    const u64 xo1 = csubk(shoup_q3(dv[e / 2].y, rs.x, rs.y, nqm), q);
+#pragma unroll
+    for (int d = 0; d < DNUM; ++d) {
+      const u64x2_t kb = kbv[e / 2][d], ka = kav[e / 2][d];
+      const u32 p = cpos + e;
+      x0[d] = (u32)d == od ? xo0 : at(d, p);
+      x1[d] = (u32)d == od ? xo1 : at(d, p + 1);
+      kb0[d] = kb.x;
+      kb1[d] = kb.y;
+      ka0[d] = ka.x;
+      ka1[d] = ka.y;
+    }
+    u64 tl, th;
+    // sum < DNUM 2q q <= 8 q^2 < q 2^64: REDC into (0, 2q), then canonical
+    dot_wide61<DNUM>(x0, kb0, tl, th);
+    const u64 a00 = csubk(mont_redc_x(tl, th, q, qi), q);
+    dot_wide61<DNUM>(x1, kb1, tl, th);
+    const u64 a01 = csubk(mont_redc_x(tl, th, q, qi), q);
+    dot_wide61<DNUM>(x0, ka0, tl, th);
+    o1[e] = csubk(mont_redc_x(tl, th, q, qi), q);
+    dot_wide61<DNUM>(x1, ka1, tl, th);
+    o1[e + 1] = csubk(mont_redc_x(tl, th, q, qi), q);
+    // out_0 = acc_0 - NTT(conv_0): both already carry P^-1
+    f0[e] = csub(a00 + q - at(od, cpos + e), q);
+    f0[e + 1] = csub(a01 + q - at(od, cpos + e + 1), q);
+  }
+  const u64 rloc = (u64)tile * H::ROWS * G::R2;
+  const u64 obase = (u64)b * ep.out_bs + (u64)r * N + rloc;
+  const u64 abase = (u64)b * ep.add_bs + (u64)r * N + rloc;
+  const u32 off = crow * G::R2 + cpos;
+  auto emit = [&](u64* out, const u64* add, const u64 (&f)[CW]) {
+    const FinishView fv{out + obase, nullptr, add ? add + abase : nullptr, 0, q, {0, 0},
+                        ep.add_gal, (u32)rloc, (u32)LOGN, 1u};
+    const gptr_u128 o = (gptr_u128)(out + obase + off);
+#pragma unroll
+    for (int e = 0; e < CW; e += 2) o[e / 2] = fv.plus(u64x2_t{f[e], f[e + 1]}, off + e);
+  };
+  emit(ks0, ep.add0, f0);
+  const u32 c1 = DNUM < 4 ? (u32)DNUM : 0u;  // conv_1's slot
+  if constexpr (DNUM == 4) {
+    __syncthreads();  // every wave's combine reads are done
+    if (grp == 0) row_fwd(conv1, 0u, FinC{});
+    __syncthreads();
+  }
+  u64 f1[CW];
+#pragma unroll
+  for (int e = 0; e < CW; ++e) f1[e] = csub(o1[e] + q - at(c1, cpos + e), q);
+  emit(ks1, ep.add1, f1);
 }
 
 // One workgroup per item, rounded up to a multiple of 8 so item -> XCD placement holds (surplus
@@ -1814,19 +1992,22 @@ int col_fwd_pass(const fhe_ctx* c, const u64* src, u64 sp, u64* dst, u64 dp, u32
 template <int LOGN, int HD>
 int ks_row_inner_dispatch(const fhe_ctx* c, const KsRowArgs& a, hipStream_t s) {
   using H = HmGeo<LOGN>;
-  if (int rc = check_grid((u64)a.rows * a.batch * H::TILES, H::THR, 1, 1, "ks_row_inner")) return rc;
-  const dim3 g((u32)((u64)a.rows * a.batch * H::TILES));
+  const u32 nrows = a.nrows ? a.nrows : a.rows;
+  if (int rc = check_grid((u64)nrows * a.batch * H::TILES, H::THR, 1, 1, "ks_row_inner")) return rc;
+  const dim3 g((u32)((u64)nrows * a.batch * H::TILES));
   switch (c->dnum) {
 #define D(k)                                                                                    \
   case k:                                                                                       \
     if (HD == 16 && a.mont)                                                                     \
       k_ks_row_inner<LOGN, HD, k, HD == 16><<<g, H::THR, 0, s>>>(                               \
-          a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.base0, \
-          a.base1, a.alpha, a.L, a.batch, a.pinv, a.rscale, c->d_tw_fwd, c->d_tw_inv, c->d_mods);\
+          a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.row0,   \
+          nrows, a.base0, a.base1, a.alpha, a.L, a.batch, a.pinv, a.rscale, c->d_tw_fwd,       \
+          c->d_tw_inv, c->d_mods);                                                              \
     else                                                                                        \
       k_ks_row_inner<LOGN, HD, k><<<g, H::THR, 0, s>>>(                                         \
-          a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.base0, \
-          a.base1, a.alpha, a.L, a.batch, a.pinv, a.rscale, c->d_tw_fwd, c->d_tw_inv, c->d_mods);\
+          a.acc, a.acc_ws, a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a, a.rows, a.nq, a.row0,   \
+          nrows, a.base0, a.base1, a.alpha, a.L, a.batch, a.pinv, a.rscale, c->d_tw_fwd,       \
+          c->d_tw_inv, c->d_mods);                                                              \
     break;
     D(1) D(2) D(3) D(4)
 #undef D
@@ -1964,6 +2145,48 @@ int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s)
       return rc;                                                                               \
     FHE_HIP_CHECK(hipGetLastError());                                                         \
     return kOk;
+    FHE_LOGN_CASES(X)
+#undef X
+  }
+  set_error("unsupported log_n");
+  return kUnsupported;
+}
+
+namespace {
+template <int LOGN>
+int ks_row_fin_dispatch(const fhe_ctx* c, const KsFinArgs& a, hipStream_t s) {
+  using H = HmGeo<LOGN>;
+  if (int rc = check_grid((u64)a.nq * a.batch * H::TILES, H::THR, 1, 1, "ks_row_fin")) return rc;
+  const dim3 g((u32)((u64)a.nq * a.batch * H::TILES));
+  switch (c->dnum) {
+#define D(k)                                                                                     \
+  case k:                                                                                        \
+    k_ks_row_fin<LOGN, k><<<g, H::THR, 0, s>>>(a.ext, a.ext_ds, a.d2_own, a.evk_b, a.evk_a,     \
+                                               a.rows, a.nq, a.base0, a.alpha, a.L, a.batch,     \
+                                               a.rscale, a.conv, a.ks0, a.ks1, a.ep, c->d_tw_fwd, \
+                                               c->d_mods);                                       \
+    break;
+    D(1) D(2) D(3) D(4)
+#undef D
+    default:
+      set_error("ks_row_fin: dnum > 4");
+      return kUnsupported;
+  }
+  FHE_HIP_CHECK(hipGetLastError());
+  return kOk;
+}
+}  // namespace
+
+int launch_ks_row_fin(const fhe_ctx* c, const KsFinArgs& a, hipStream_t s) {
+  if ((u64)a.nq * a.batch == 0) return kOk;
+  if (c->wide || !c->lz16) {
+    set_error("ks_row_fin: needs an lz16 context (every modulus below 2^60)");
+    return kUnsupported;
+  }
+  switch (c->log_n) {
+#define X(n) \
+  case n:    \
+    return ks_row_fin_dispatch<n>(c, a, s);
     FHE_LOGN_CASES(X)
 #undef X
   }

@@ -45,10 +45,10 @@ __global__ __launch_bounds__(kThreads) void k_tensor_ntt(u64* __restrict__ d,
 
 size_t mul_relin_workspace_bytes(const fhe_ctx* c, u32 batch) {
   const size_t ln = (size_t)c->L * c->n * sizeof(u64);
-  // d0, d1 [2], relinearised ct before the rescale [2] (d2 parks there until the key-switch's
-  // finish), the rescale's own [2 L N] workspace, the key-switch's workspace (its tail holds
-  // INTT(d2))
-  return (size_t)batch * ln * (2 + 2) + rescale_workspace_bytes(c, 2 * batch, c->L) +
+  // d0, d1 [2], relinearised ct before the rescale [2], d2 [1] (the key-switch's finish may run in
+  // the same kernel as its reads of d2, k_ks_row_fin, so d2 cannot park in the output), the
+  // rescale's own [2 L N] workspace, the key-switch's workspace (its tail holds INTT(d2))
+  return (size_t)batch * ln * (2 + 2 + 1) + rescale_workspace_bytes(c, 2 * batch, c->L) +
          keyswitch_workspace_bytes(c, c->L, batch);
 }
 
@@ -77,14 +77,12 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   }
   u64* d = static_cast<u64*>(ws);        // [batch][2][L][N]: d0, d1
   u64* rl = d + 2 * batch * ln;          // [batch][2][L][N] relinearised, before the rescale
-  u64* rws = rl + 2 * batch * ln;        // rescale workspace
+  u64* d2 = rl + 2 * batch * ln;         // [batch][L][N] d2, NTT form, the key-switch's input
+  u64* rws = d2 + batch * ln;            // rescale workspace
   u64* kws = reinterpret_cast<u64*>(reinterpret_cast<char*>(rws) +
                                     rescale_workspace_bytes(c, 2 * batch, L));
   if (int rc = check_grid(n / kThreads, kThreads, L, batch, "tensor_ntt")) return rc;
   const dim3 g((u32)(n / kThreads), L, batch);
-  // d2 (NTT form) as a contiguous [batch][L][N] operand for the key-switch: parked in the
-  // relinearised-ct buffer, which is free until the combine
-  u64* d2 = rl;
   k_tensor_ntt<<<g, kThreads, 0, s>>>(d, d2, a, b, L, c->log_n, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
   prof_mark(s, "tensor_ntt");
@@ -100,8 +98,7 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   CAll call = CAll::contiguous(c_all, L, n);
   call.scaled = prep;
   // the relinearised ciphertext (d0 + ks0, d1 + ks1) straight out of the ModDown finish
-  // ([batch][2][L][N] outputs and addends, 2 L N apart per ciphertext); d2's slot in rl is dead
-  // by then (read by the INTT and the inner product only)
+  // ([batch][2][L][N] outputs and addends, 2 L N apart per ciphertext)
   u64* dst = rescale ? rl : out;
   KsEpilogue ep;
   ep.out_bs = 2 * ln;

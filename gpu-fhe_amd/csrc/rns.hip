@@ -541,11 +541,27 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   }
   // the fused row kernel also runs the first (row) pass of ModDown's INTT on the special rows
   const bool row_pinv = fused && fused_down;
+  // With P^-1 in the constants the Q rows wait for ModDown's conversion and finish in the same
+  // workgroup (k_ks_row_fin): the row kernel covers only the special rows first, their column
+  // inverse runs in place in the accumulators (the ext region stays intact for the Q rows), and
+  // neither the accumulators' Q rows nor k_moddown_row's pass over them touch HBM.
+  // (not when an output overlaps d2_own: the finish kernel writes outputs while other
+  // workgroups still read d2_own)
+  const u64 out_words = (u64)(batch - 1) * ep.out_bs + (u64)nlimbs * n;
+  const u64 d2_words = (u64)batch * nlimbs * n;
+  auto overlaps = [&](const u64* o) {
+    return o < d2_own + d2_words && d2_own < o + out_words;
+  };
+  const bool qfin = pscale && row_pinv && !overlaps(ks0) && !overlaps(ks1);
   if (fused) {
     KsRowArgs ka{acc, acc_ws, ext, B * rn, d2_own, evk_b, evk_a, rows, nlimbs, limb0, L,
                  alpha, L, batch, mont_ext};
     ka.pinv = row_pinv ? 1u : 0u;
     ka.rscale = pscale ? c->d_rpinv : nullptr;
+    if (qfin) {
+      ka.row0 = nlimbs;
+      ka.nrows = K;
+    }
     if ((rc = launch_ks_row_inner(c, ka, s))) return rc;
   }
   const dim3 gi((u32)(n / kThreads), rows);
@@ -569,18 +585,26 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   if (fused_down) {
     // the INTT writes y = [x_k (P^_k)^-1]_{p_k} straight into [2 batch][K][N] (its last stage
     // folds N^-1 (P^_k)^-1, c->d_nfold_down): no separate scaling pass
-    u64* ydn = hoist ? hoist->ydn : ext;
-    if ((rc = row_pinv ? launch_ntt_col_inv(c, accp, rn, ydn, (u64)K * n, 2 * batch, L, K, s,
+    u64* ydn = qfin ? accp : hoist ? hoist->ydn : ext;
+    const u64 yps = qfin ? rn : (u64)K * n;  // poly stride of the scaled P rows
+    if ((rc = row_pinv ? launch_ntt_col_inv(c, accp, rn, ydn, yps, 2 * batch, L, K, s,
                                             c->d_nfold_down, ks_split30(c))
-                       : launch_ntt_strided(c, false, accp, rn, ydn, (u64)K * n, 2 * batch, L, K,
+                       : launch_ntt_strided(c, false, accp, rn, ydn, yps, 2 * batch, L, K,
                                             s, c->d_nfold_down, ks_split30(c))))
       return rc;
     prof_mark(s, "ks_moddown_conv");
-    const ModUpColArgs md{ydn, (u64)K * n, {0, n, 2 * n, 3 * n}, conv, (u64)nlimbs * n, K, nlimbs,
+    const ModUpColArgs md{ydn, yps, {0, n, 2 * n, 3 * n}, conv, (u64)nlimbs * n, K, nlimbs,
                           nlimbs, 0, nlimbs, limb0, 0, 2 * batch,
                           pscale ? c->d_moddown_hat_wp : c->d_moddown_hat_w, M};
     if ((rc = launch_modup_col(c, md, s))) return rc;
     prof_mark(s, "ks_moddown_col");
+    if (qfin) {
+      const KsFinArgs fa{ext, B * rn, d2_own, evk_b, evk_a, rows, nlimbs, limb0, alpha, L, batch,
+                         c->d_rpinv, conv, ks0, ks1, ep};
+      if ((rc = launch_ks_row_fin(c, fa, s))) return rc;
+      prof_mark(s, "ks_row_fin");
+      return kOk;
+    }
     ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch, ep};
     da.prescaled = pscale ? 1u : 0u;
     if ((rc = launch_moddown_row(c, da, s))) return rc;
