@@ -1720,7 +1720,7 @@ __global__ FHE_KATTR void k_ks_row_fin(const u64* __restrict__ ext, u64 ext_ds,
   const u32 crow = cpos0 / G::R2, cpos = cpos0 % G::R2;
   const u64 orow = (u64)(tile * H::ROWS + crow) * G::R2 + cpos;  // position within the poly
   const u64 okey = (u64)r * N + orow;
-  const u64* lrow = lds + crow * H::ROWW;
+  u64* lrow = lds + crow * H::ROWW;
   u64x2_t kbv[CW / 2][DNUM], kav[CW / 2][DNUM], dv[CW / 2];
 #pragma unroll
   for (int e = 0; e < CW; e += 2) {
@@ -1781,15 +1781,21 @@ __global__ FHE_KATTR void k_ks_row_fin(const u64* __restrict__ ext, u64 ext_ds,
     for (int e = 0; e < CW; e += 2) o[e / 2] = fv.plus(u64x2_t{f[e], f[e + 1]}, off + e);
   };
   emit(ks0, ep.add0, f0);
-  const u32 c1 = DNUM < 4 ? (u32)DNUM : 0u;  // conv_1's slot
+  u64 f1[CW];
   if constexpr (DNUM == 4) {
-    __syncthreads();  // every wave's combine reads are done
+    // acc_1 waits in slot 1 (free once every combine read is done) while wave 0 runs conv_1's
+    // row pass into slot 0: no registers held across that pass
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < CW; ++e) lrow[1 * G::RS + (cpos + e) + ((cpos + e) >> 4)] = o1[e];
     if (grp == 0) row_fwd(conv1, 0u, FinC{});
     __syncthreads();
-  }
-  u64 f1[CW];
 #pragma unroll
-  for (int e = 0; e < CW; ++e) f1[e] = csub(o1[e] + q - at(c1, cpos + e), q);
+    for (int e = 0; e < CW; ++e) f1[e] = csub(at(1, cpos + e) + q - at(0, cpos + e), q);
+  } else {
+#pragma unroll
+    for (int e = 0; e < CW; ++e) f1[e] = csub(o1[e] + q - at(DNUM, cpos + e), q);
+  }
   emit(ks1, ep.add1, f1);
 }
 
