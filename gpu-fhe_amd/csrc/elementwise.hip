@@ -3,7 +3,7 @@
 //
 // Two entry families:
 //  * context kernels: canonical residues in [0, q_l) for the context's limb moduli, layout
-//    [polys][nlimbs][N]; kU 16-byte loads per operand per lane (HBM-bound, 24 B/elem);
+//    [polys][nlimbs][N]; kU 16-byte non-temporal loads per operand per lane (HBM-bound, 24 B/elem);
 //  * generic kernels for the reference-shaped Python API: any u64 (or signed i64) inputs, any
 //    modulus 2 <= q < 2^64, one modulus per row (scalar MOD or a (L, 1) MOD column); results
 //    equal Python's exact `(a op b) % MOD` (the object-dtype semantics).
@@ -24,36 +24,41 @@ __device__ __forceinline__ u64 op_canon(int op, u64 a, u64 b, const ModParams& m
 // 16-byte pairs per lane per operand.  Rows beyond the grid's y extent loop.  kU = 1 measured best
 // (bench --workload vec, same-box: 1 / 2 / 4 / 8 -> 2.32 / 2.28 / 2.17 / 2.00 e11 coeff-op/s):
 // more, shorter workgroups keep more loads in flight than more loads per lane.
+// Every operand word is touched once, so loads and stores are non-temporal (streamed past the
+// caches) and workgroups are 2 waves: same-box, 3 repetitions, 2.41-2.47 e11 coeff-op/s with cached
+// accesses at 256 threads -> 2.69-2.74 e11 (+11 %; non-temporal stores alone +1 %, loads alone
+// +3 %, both at 512 / 256 threads 2.65-2.70 e11; profiles/r05_vec_nontemporal_ab*.txt).
 constexpr int kU = 1;
+constexpr int kVecThreads = 128;
+typedef u64 vu64x2 __attribute__((ext_vector_type(2)));
 template <int OP>
-__global__ __launch_bounds__(kThreads) void k_vec_ctx(u64* __restrict__ out,
+__global__ __launch_bounds__(kVecThreads) void k_vec_ctx(u64* __restrict__ out,
                                                       const u64* __restrict__ a,
                                                       const u64* __restrict__ b, u32 row_pairs,
                                                       u32 rows, u32 nlimbs, u32 limb0,
                                                       const ModParams* __restrict__ mods) {
-  const u32 p0 = blockIdx.x * (kThreads * kU) + threadIdx.x;
+  const u32 p0 = blockIdx.x * (kVecThreads * kU) + threadIdx.x;
   for (u32 row = blockIdx.y; row < rows; row += gridDim.y) {
     const ModParams m = mods[limb0 + row % nlimbs];
     const u64 base = (u64)row * row_pairs;
-    const ulonglong2* pa = reinterpret_cast<const ulonglong2*>(a) + base;
-    const ulonglong2* pb = reinterpret_cast<const ulonglong2*>(b) + base;
-    ulonglong2* po = reinterpret_cast<ulonglong2*>(out) + base;
-    ulonglong2 x[kU], y[kU];
+    const vu64x2* pa = reinterpret_cast<const vu64x2*>(a) + base;
+    const vu64x2* pb = reinterpret_cast<const vu64x2*>(b) + base;
+    vu64x2* po = reinterpret_cast<vu64x2*>(out) + base;
+    vu64x2 x[kU], y[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const u32 i = p0 + u * kThreads;
+      const u32 i = p0 + u * kVecThreads;
       if (i < row_pairs) {
-        x[u] = pa[i];
-        y[u] = pb[i];
+        x[u] = __builtin_nontemporal_load(pa + i);
+        y[u] = __builtin_nontemporal_load(pb + i);
       }
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const u32 i = p0 + u * kThreads;
+      const u32 i = p0 + u * kVecThreads;
       if (i < row_pairs) {
-        // (non-temporal stores measured neutral over the three operators: they only move time
-        // from one kernel to the next)
-        po[i] = ulonglong2{op_canon(OP, x[u].x, y[u].x, m), op_canon(OP, x[u].y, y[u].y, m)};
+        const vu64x2 r = {op_canon(OP, x[u].x, y[u].x, m), op_canon(OP, x[u].y, y[u].y, m)};
+        __builtin_nontemporal_store(r, po + i);
       }
     }
   }
@@ -107,11 +112,12 @@ int launch_vec_ctx(const fhe_ctx* c, int op, u64* out, const u64* a, const u64* 
     return kInvalid;
   }
   const u32 rows = (u32)rows64, row_pairs = (u32)(c->n / 2);  // N >= 2^10: whole pairs per row
-  const dim3 g((row_pairs + kThreads * kU - 1) / (kThreads * kU), rows < 65535 ? rows : 65535);
+  constexpr u32 kT = kVecThreads;
+  const dim3 g((row_pairs + kT * kU - 1) / (kT * kU), rows < 65535 ? rows : 65535);
   switch (op) {
-    case kAdd: k_vec_ctx<kAdd><<<g, kThreads, 0, s>>>(out, a, b, row_pairs, rows, nlimbs, limb0, c->d_mods); break;
-    case kSub: k_vec_ctx<kSub><<<g, kThreads, 0, s>>>(out, a, b, row_pairs, rows, nlimbs, limb0, c->d_mods); break;
-    case kMul: k_vec_ctx<kMul><<<g, kThreads, 0, s>>>(out, a, b, row_pairs, rows, nlimbs, limb0, c->d_mods); break;
+    case kAdd: k_vec_ctx<kAdd><<<g, kT, 0, s>>>(out, a, b, row_pairs, rows, nlimbs, limb0, c->d_mods); break;
+    case kSub: k_vec_ctx<kSub><<<g, kT, 0, s>>>(out, a, b, row_pairs, rows, nlimbs, limb0, c->d_mods); break;
+    case kMul: k_vec_ctx<kMul><<<g, kT, 0, s>>>(out, a, b, row_pairs, rows, nlimbs, limb0, c->d_mods); break;
     default: set_error("bad vec op"); return kInvalid;
   }
   FHE_HIP_CHECK(hipGetLastError());
