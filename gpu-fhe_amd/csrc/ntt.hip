@@ -1840,7 +1840,25 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
   const u64 ic = pl * G::TILES_C;
   if (int rc = check_grid(item_blocks(ic), G::THR_C, 1, 1, "ntt")) return rc;
   if (int rc = check_grid(item_blocks(pl * G::TILES_R), G::THR_R, 1, 1, "ntt")) return rc;
-  if (fwd) {
+  // Transforms far larger than the Infinity Cache (configs[4]: 32 GiB per call) stream every
+  // access (non-temporal loads and stores in both passes): the intermediate is evicted before the
+  // row pass reads it anyway.  configs[4] forward 1.139-1.140 -> 1.204-1.205 M NTT/s same-box
+  // (+5.7 %; only the column pass's source / the row pass's output streamed: +3 %;
+  // profiles/r05_ntt_stream_ab.txt).  Smaller ones stay cached: their second pass re-reads the
+  // first pass's output from the Infinity Cache (non-temporal there: -5 ... -8 %, round 3).
+  const bool stream = pl * G::R1 * G::R2 * 8 > (1ull << 30);
+  if (fwd && stream) {
+    k_ntt_col<LOGN, true, HD, true, true>
+        <<<item_grid(ic),
+           G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd,
+                             c->d_nfold, c->d_mods);
+    prof_mark(s, "ntt_col_fwd");
+    const u64 ir = pl * G::TILES_R;
+    k_ntt_row<LOGN, true, HD, true, true>
+        <<<item_grid(ir), G::THR_R,
+           0, s>>>(dst, dst, nlimbs, limb0, pd, (u32)ir, c->d_tw_fwd, c->d_mods);
+    prof_mark(s, "ntt_row_fwd");
+  } else if (fwd) {
     k_ntt_col<LOGN, true, HD>
         <<<item_grid(ic),
            G::THR_C, 0, s>>>(src, nullptr, dst, nlimbs, limb0, pm, (u32)ic, c->d_tw_fwd,
