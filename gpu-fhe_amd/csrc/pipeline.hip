@@ -15,30 +15,41 @@
 namespace fhe {
 namespace {
 
-constexpr int kThreads = 256;
 
 // a, b [batch][2][L][N] NTT form, canonical -> d0, d1 into d [batch][2][L][N] and d2 into its own
-// contiguous [batch][L][N] (the key-switch's operand, no gather copy).  Grid: x over coefficients,
-// y = limb, z = ciphertext.
-__global__ __launch_bounds__(kThreads) void k_tensor_ntt(u64* __restrict__ d,
-                                                         u64* __restrict__ d2,
-                                                         const u64* __restrict__ a,
-                                                         const u64* __restrict__ b, u32 L,
-                                                         u32 log_n,
-                                                         const ModParams* __restrict__ mods) {
+// contiguous [batch][L][N] (the key-switch's operand, no gather copy).  Grid: x over coefficient
+// pairs (16-byte accesses), y = limb, z = ciphertext.  a, b are read once and d0, d1 are read back
+// only by the key-switch's finish, long after they left the caches: non-temporal; d2 stays cached
+// for the INTT that reads it next.
+typedef u64 vu64x2 __attribute__((ext_vector_type(2)));
+constexpr int kTensorThreads = 128;
+__global__ __launch_bounds__(kTensorThreads) void k_tensor_ntt(u64* __restrict__ d,
+                                                               u64* __restrict__ d2,
+                                                               const u64* __restrict__ a,
+                                                               const u64* __restrict__ b, u32 L,
+                                                               u32 log_n,
+                                                               const ModParams* __restrict__ mods) {
   const u64 n = 1ull << log_n, ln = (u64)L * n;
-  const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u64 c = 2 * ((u64)blockIdx.x * blockDim.x + threadIdx.x);
   const u32 l = blockIdx.y;
   const u64 bt = blockIdx.z;
   const ModParams m = mods[l];
   const u64 off = bt * 2 * ln + (u64)l * n + c;
-  const u64 a0 = a[off], a1 = a[off + ln], b0 = b[off], b1 = b[off + ln];
-  const u128 t0 = (u128)a0 * b0, t2 = (u128)a1 * b1;
-  const u128 t1 = (u128)a0 * b1 + (u128)a1 * b0;
+  auto ld = [](const u64* p) { return __builtin_nontemporal_load(reinterpret_cast<const vu64x2*>(p)); };
+  const vu64x2 a0 = ld(a + off), a1 = ld(a + off + ln), b0 = ld(b + off), b1 = ld(b + off + ln);
+  vu64x2 o0, o1, o2;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const u128 t0 = (u128)a0[h] * b0[h], t2 = (u128)a1[h] * b1[h];
+    const u128 t1 = (u128)a0[h] * b1[h] + (u128)a1[h] * b0[h];
+    o0[h] = reduce128_any((u64)t0, (u64)(t0 >> 64), m);
+    o1[h] = reduce128_any((u64)t1, (u64)(t1 >> 64), m);
+    o2[h] = reduce128_any((u64)t2, (u64)(t2 >> 64), m);
+  }
   u64* o = d + bt * 2 * ln + (u64)l * n + c;
-  o[0] = reduce128_any((u64)t0, (u64)(t0 >> 64), m);
-  o[ln] = reduce128_any((u64)t1, (u64)(t1 >> 64), m);
-  d2[bt * ln + (u64)l * n + c] = reduce128_any((u64)t2, (u64)(t2 >> 64), m);
+  __builtin_nontemporal_store(o0, reinterpret_cast<vu64x2*>(o));
+  __builtin_nontemporal_store(o1, reinterpret_cast<vu64x2*>(o + ln));
+  *reinterpret_cast<vu64x2*>(d2 + bt * ln + (u64)l * n + c) = o2;
 }
 
 }  // namespace
@@ -81,9 +92,10 @@ int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, con
   u64* rws = d2 + batch * ln;            // rescale workspace
   u64* kws = reinterpret_cast<u64*>(reinterpret_cast<char*>(rws) +
                                     rescale_workspace_bytes(c, 2 * batch, L));
-  if (int rc = check_grid(n / kThreads, kThreads, L, batch, "tensor_ntt")) return rc;
-  const dim3 g((u32)(n / kThreads), L, batch);
-  k_tensor_ntt<<<g, kThreads, 0, s>>>(d, d2, a, b, L, c->log_n, c->d_mods);
+  const u64 tb = n / 2 / kTensorThreads;  // N >= 2^10: whole blocks of coefficient pairs
+  if (int rc = check_grid(tb, kTensorThreads, L, batch, "tensor_ntt")) return rc;
+  const dim3 g((u32)tb, L, batch);
+  k_tensor_ntt<<<g, kTensorThreads, 0, s>>>(d, d2, a, b, L, c->log_n, c->d_mods);
   FHE_HIP_CHECK(hipGetLastError());
   prof_mark(s, "tensor_ntt");
   // d2 = d[b][2]: gather to a contiguous [batch][L][N] operand for the key-switch (its INTT lands
