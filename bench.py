@@ -61,9 +61,17 @@ def parse():
                          "exact wide-modulus butterflies)")
     ap.add_argument("--ks-chunks", type=int, default=0,
                     help="keyswitch: all-gather chunks per batch (0 = 1 at N = 1, 4 above)")
+    ap.add_argument("--ks-groups", type=int, default=1,
+                    help="keyswitch: ciphertext groups of the hybrid partition (fhe_dist_hybrid): "
+                         "the ranks form this many groups of N / groups limb shards, each group "
+                         "key-switches its share of the batch with the all-gather inside the group "
+                         "(1 = the limb-only partition, north_star's; N = whole ciphertexts per GPU)")
     ap.add_argument("--ks-batch", type=int, default=32,
                     help="keyswitch (and the default line's key-switch leg): ciphertexts per "
                          "call, the whole job's (limbs sharded: strong scaling)")
+    ap.add_argument("--inverse", action="store_true",
+                    help="ntt-batch: time the inverse transform (configs[4]'s round trip back) "
+                         "instead of the forward")
     ap.add_argument("--no-keyswitch-leg", action="store_true",
                     help="hommult: skip the key-switch ride-along leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample budget")
@@ -832,15 +840,19 @@ def run_ntt_batch(args, world, rank):
         r = torch.randint(0, 2**62, (mine, n), generator=gen, dtype=torch.int64, device="cuda")
         x[:, l, :] = torch.remainder(r, q)
         del r
-    step = lambda: ctx.ntt_(x)  # noqa: E731  (in place: canonical in, canonical out)
+    # in place: canonical in, canonical out (the inverse is a bijection of canonical residues, so
+    # timing it on uniform inputs is the round trip's second half)
+    inv = bool(getattr(args, "inverse", False))
+    step = (lambda: ctx.intt_(x)) if inv else (lambda: ctx.ntt_(x))  # noqa: E731
     dt, kavg = timed(step, args, world, 4 * args.steps + 4)
     ntts = P * L * args.steps
     shape = {"log_n": log_n, "polys": mine, "nlimbs": L}
     per_pass = mine * L * n * 16
-    out = {"metric": "NTTs/sec, 1024 x N=2^17 x 32 RNS limbs (forward, batched); achieved HBM GB/s vs peak",
+    d = "inverse" if inv else "forward"
+    out = {"metric": f"NTTs/sec, 1024 x N=2^17 x 32 RNS limbs ({d}, batched); achieved HBM GB/s vs peak",
            "value": round(ntts / dt, 1), "unit": "NTT/s",
            "ms_per_step": round(dt / args.steps * 1e3, 4), "scaling": "strong",
-           "config": {"workload": "batched forward NTT, BASELINE configs[4]", "log_n": log_n,
+           "config": {"workload": f"batched {d} NTT, BASELINE configs[4]", "log_n": log_n,
                       "limbs": L, "polys": P, "polys_per_gpu": mine,
                       "parallelism": f"poly-shard x{world}"},
            # whole transform: read + write every coefficient once (two passes move it twice)
@@ -881,7 +893,13 @@ class KeyswitchLeg:
 
     def __init__(self, args, world, rank):
         self.world, self.rank = world, rank
-        self.shard = fdist.LimbShard(self.L, world, rank)
+        # hybrid partition (fhe_dist_hybrid): `groups` ciphertext groups of g limb shards; groups = 1
+        # is the limb-only partition (every rank one limb shard of the whole batch)
+        self.groups = max(1, getattr(args, "ks_groups", 1) or 1)
+        if world % self.groups:
+            raise SystemExit(f"--ks-groups {self.groups} does not divide {world} ranks")
+        self.g = world // self.groups
+        self.shard = fdist.LimbShard(self.L, self.g, rank % self.g)
         self.log_n = args.log_n
         n = 1 << args.log_n
         self.ctx = ctx = fc.Context(args.log_n, L=self.L, K=self.K, dnum=self.DNUM)
@@ -892,24 +910,31 @@ class KeyswitchLeg:
         self.evk_b = uniform_limbs(gen, [allm[r] for r in rows], (self.DNUM,), n)
         self.evk_a = uniform_limbs(gen, [allm[r] for r in rows], (self.DNUM,), n)
         self.B = args.ks_batch
-        self.d2 = uniform_limbs(gen, ctx.moduli[self.shard.lo:self.shard.hi], (self.B,), n)
-        self.chunks = args.ks_chunks or (1 if world == 1 else 4)
+        self.chunks = args.ks_chunks or (1 if self.g == 1 else 4)
+        self.hybrid = fdist.hybrid_plan(self.L, self.log_n, world, self.groups, rank, self.B,
+                                        self.chunks)
+        self.my_batch = self.hybrid.batch  # this rank's group's ciphertexts
+        self.d2 = uniform_limbs(gen, ctx.moduli[self.shard.lo:self.shard.hi], (self.my_batch,), n)
         self.live_pmc = world == 1 and rank == 0 and not args.no_pmc
+        # the group's torch.distributed sub-group (every rank creates all of them, in order);
+        # None: the group is the world (groups = 1) or one rank (g = 1)
+        self.group = fdist.hybrid_groups(world, self.groups) if 1 < self.groups < world else None
         # the native path needs one GPU per rank (RCCL refuses two ranks on one device); the
         # gloo rehearsal of several ranks on one GPU takes the torch.distributed form instead
         # (fhecore.dist.sharded_keyswitch: INTT, one all_gather through the host, local step)
         self.native = world == 1 or torch.distributed.get_backend() == "nccl"
         if self.native:
-            self.comm = fdist.RcclComm()
+            self.comm = fdist.RcclComm(group=self.group, local=self.g == 1)
             self.ws = ctx.workspace(load().fhe_keyswitch_dist_workspace(
-                ctx.handle, self.comm.handle, self.B, self.chunks))
+                ctx.handle, self.comm.handle, max(self.my_batch, 1), self.chunks))
 
     def step(self):
         if self.native:
             self.ctx.keyswitch_dist(self.comm, self.d2, self.evk_b, self.evk_a,
                                     chunks=self.chunks, workspace=self.ws)
         else:
-            fdist.sharded_keyswitch(self.ctx, self.d2, self.evk_b, self.evk_a, self.shard)
+            fdist.sharded_keyswitch(self.ctx, self.d2, self.evk_b, self.evk_a, self.shard,
+                                    group=self.group)
 
     def run(self, targs, valu=False):
         L, K, dnum, B, world = self.L, self.K, self.DNUM, self.B, self.world
@@ -926,7 +951,10 @@ class KeyswitchLeg:
                "config": {"workload": "hybrid key-switch, BASELINE configs[3] (fhe_keyswitch_dist)",
                           "log_n": self.log_n, "L": L, "K": K, "dnum": dnum, "batch": B,
                           "chunks": self.chunks if self.native else 1, "scaling": "strong",
-                          "parallelism": f"rns-limb-shard x{world}, " + (
+                          "ks_groups": self.groups,
+                          "parallelism": (f"rns-limb-shard x{world}, " if self.groups == 1 else
+                                          f"hybrid: {self.groups} ciphertext groups x "
+                                          f"rns-limb-shard x{self.g}, ") + (
                               "RCCL all-gather in libfhecore (fhe_keyswitch_dist)" if self.native
                               else "torch.distributed all_gather (gloo, host-staged; "
                                    "fhecore.dist.sharded_keyswitch)")},
@@ -936,15 +964,20 @@ class KeyswitchLeg:
                "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
                "roofline": roofline("keyswitch (whole, per GPU)", alg // world, ms_per_ks,
                                     {"log_n": self.log_n, "L": L, "world": world})}
-        plan = fdist.dist_plan(L, self.log_n, world, self.rank, B, self.chunks if self.native else 1)
-        res["gather_bytes_per_chunk"] = plan.block_words * 8 * world  # what each rank ends up with
+        plan = fdist.hybrid_plan(L, self.log_n, world, self.groups, self.rank, B,
+                                 self.chunks if self.native else 1).plan
+        # what each rank ends up with (its group's g blocks; nothing is gathered at g = 1)
+        res["gather_bytes_per_chunk"] = plan.block_words * 8 * self.g if self.g > 1 else 0
         # integer-ALU roofline of one key-switch on this rank, butterflies only: INTT of the own
         # d2 limbs; ModUp: every digit's extended rows = dnum (nl + K) - nl forward NTTs; ModDown:
         # INTT of the 2 K special rows, forward NTT of the 2 nl converted rows
+        # (per job key-switch: this rank processes my_batch of the job's B ciphertexts)
         nl, full = self.shard.nlimbs, (n // 2) * self.log_n
+        share = self.my_batch / B
         res["roofline_alu"] = roofline_alu(
             "keyswitch (whole, per GPU; NTT butterflies only)",
-            (dnum * (nl + K) + nl) * full, (nl + 2 * K) * full, ms_per_ks)
+            round((dnum * (nl + K) + nl) * full * share), round((nl + 2 * K) * full * share),
+            ms_per_ks)
         # ... and by VALU instruction issue, which counts everything the kernels execute (base
         # conversion products, inner products, reductions, addressing): SQ_INSTS_VALU of each
         # key-switch kernel at this shape from a rocprofv3 --pmc pass over a child process
@@ -1265,8 +1298,11 @@ def dist_check(world, rank, hm_ctx=None, ks_leg=None, seed=4321):
         del a, b
     if ks_leg is not None:
         ctx, shard = ks_leg.ctx, ks_leg.shard
-        # a batch of 2 per chunk so that the chunked own-stream path (chunks > 1) runs as timed
-        B = 2 * ks_leg.chunks
+        # a batch of 2 per chunk per ciphertext group so that the chunked own-stream path
+        # (chunks > 1) runs as timed; each rank checks its group's ciphertexts
+        B = 2 * ks_leg.chunks * ks_leg.groups
+        h = fdist.hybrid_plan(ctx.L, ctx.log_n, world, ks_leg.groups, rank, B, ks_leg.chunks)
+        mine = slice(h.batch0, h.batch0 + h.batch)
         d2 = uniform_limbs(gen, ctx.moduli, (B,), ctx.n)
         kb = uniform_limbs(gen, ctx.all_moduli, (ks_leg.DNUM,), ctx.n)
         ka = uniform_limbs(gen, ctx.all_moduli, (ks_leg.DNUM,), ctx.n)
@@ -1275,9 +1311,12 @@ def dist_check(world, rank, hm_ctx=None, ks_leg=None, seed=4321):
                                                       chunks=ks_leg.chunks)
             how = f"fhe_keyswitch_dist over RCCL, {ks_leg.chunks} chunk(s)"
         else:
-            fn = lambda d, eb, ea: fdist.sharded_keyswitch(ctx, d, eb, ea, shard)  # noqa: E731
+            fn = lambda d, eb, ea: fdist.sharded_keyswitch(ctx, d, eb, ea, shard,  # noqa: E731
+                                                           group=ks_leg.group)
             how = "torch.distributed all_gather form (gloo)"
-        bad += check_keyswitch_shard(ctx, shard, ks_leg.K, d2, kb, ka, fn)
+        if ks_leg.groups > 1:
+            how += f", hybrid: {ks_leg.groups} ciphertext groups x {ks_leg.g} limb shards"
+        bad += check_keyswitch_shard(ctx, shard, ks_leg.K, d2[mine].contiguous(), kb, ka, fn)
         parts.append(f"key-switch ({how}, batch {B}, L={ctx.L}, K={ctx.K})")
         del d2, kb, ka
     torch.cuda.synchronize()

@@ -300,6 +300,11 @@ int fhe_keyswitch(const fhe_ctx* c, uint64_t* ks0, uint64_t* ks1, const uint64_t
   if (rc) return rc;
   if (batch == 0) return kOk;
   const uint64_t ct_words = (uint64_t)c->L * c->n;
+  // the whole batch at once: a pass must not overwrite a later pass's d2 (per-pass checks in the
+  // launcher would miss an output shifted onto the next pass's input)
+  if ((rc = ks_check_alias(ks0, ks1, d2, batch * ct_words, batch * ct_words, true,
+                           "fhe_keyswitch")))
+    return rc;
   const uint32_t pass = ks_pass_batch(c, batch);  // Infinity-Cache-sized passes
   const size_t bytes = keyswitch_workspace_bytes(c, c->L, pass);
   if ((rc = ensure_ws(c, bytes, &ws, hs(s)))) return rc;
@@ -358,8 +363,11 @@ int fhe_rotate(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t gal
                fhe_stream_t s) {
   int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_rotate");
   if (rc) return rc;
-  if (out == in && batch) {
-    set_error("fhe_rotate: out must not alias in");
+  // the finish reads c0 through sigma (any word of its row block) while other workgroups write
+  // out: any overlap of the two [batch][2][L][N] spans races, not just out == in
+  const uint64_t span = (uint64_t)batch * 2 * c->L * c->n;
+  if (spans_overlap(out, span, in, span)) {
+    set_error("fhe_rotate: out must not overlap in");
     return kInvalid;
   }
   if ((rc = ensure_ws(c, rotate_workspace_bytes(c, ks_pass_batch(c, batch)), &ws, hs(s)))) return rc;

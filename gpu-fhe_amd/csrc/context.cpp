@@ -117,7 +117,7 @@ int ctx_destroy(fhe_ctx* c) {
   (void)hipSetDevice(c->device);
   for (auto& t : c->bc_tables) (void)hipFree(t.second);
   for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_inv, (void*)c->d_nfold, (void*)c->d_nfold_down, (void*)c->d_nfold_up,
-                    (void*)c->d_modup_inv, (void*)c->d_modup_hat, (void*)c->d_modup_hat_r, (void*)c->d_moddown_inv,
+                    (void*)c->d_modup_inv, (void*)c->d_modup_hat, (void*)c->d_moddown_inv,
                     (void*)c->d_moddown_hat, (void*)c->d_modup_hat_w, (void*)c->d_modup_hat_rw,
                     (void*)c->d_moddown_hat_w, (void*)c->d_modup_hat_rwp,
                     (void*)c->d_moddown_hat_wp, (void*)c->d_rpinv, (void*)c->d_pinv, (void*)c->d_rs_tab,

@@ -278,6 +278,10 @@ int fhe_keyswitch_dist(const fhe_ctx* ctx, fhe_comm_t comm, uint64_t* ks0, uint6
   if ((rc = fhe_dist_plan_make(&p, ctx->L, ctx->log_n, (u32)comm->nranks, (u32)comm->rank, batch,
                                chunks)))
     return rc;
+  // whole batch: chunk k's outputs must not land on a later chunk's d2 (fhecore.h aliasing rule)
+  const u64 own_words = (u64)batch * p.nlimbs * ctx->n;
+  if ((rc = ks_check_alias(ks0, ks1, d2_own, own_words, own_words, true, "fhe_keyswitch_dist")))
+    return rc;
   if ((rc = ensure_ws(ctx, dist_workspace(ctx, p, p.nlimbs), &ws, s))) return rc;
   u64* gather = static_cast<u64*>(ws);  // [nc][G][cb][cw][N]
   void* kws = gather + p.gather_words;
@@ -351,6 +355,10 @@ int fhe_keyswitch_dist_loopback(const fhe_ctx* ctx, uint32_t ranks, uint64_t* co
       set_error("fhe_keyswitch_dist_loopback: null pointer for rank " + std::to_string(r));
       return kInvalid;
     }
+    const u64 own_words = (u64)batch * plan[r].nlimbs * ctx->n;
+    if ((rc = ks_check_alias(ks0[r], ks1[r], d2_own[r], own_words, own_words, true,
+                             "fhe_keyswitch_dist_loopback")))
+      return rc;
   }
   if ((rc = ensure_ws(ctx, fhe_keyswitch_dist_loopback_workspace(ctx, ranks, batch, chunks), &ws,
                       s)))
@@ -367,6 +375,68 @@ int fhe_keyswitch_dist_loopback(const fhe_ctx* ctx, uint32_t ranks, uint64_t* co
       if ((rc = dist_ks_chunk(ctx, plan[r], k, ks0[r], ks1[r], d2_own[r], evk_b[r], evk_a[r],
                               gather, kws, s)))
         return rc;
+  return kOk;
+}
+
+// ---- hybrid partition: `groups` ciphertext groups x g = ranks / groups limb shards -----------
+int fhe_dist_hybrid_make(fhe_dist_hybrid* h, uint32_t L, uint32_t log_n, uint32_t ranks,
+                         uint32_t groups, uint32_t rank, uint32_t batch, uint32_t chunks) {
+  if (!h || groups == 0 || ranks == 0 || ranks % groups || rank >= ranks) {
+    set_error("fhe_dist_hybrid_make: need groups | ranks and 0 <= rank < ranks");
+    return kInvalid;
+  }
+  *h = fhe_dist_hybrid{};
+  h->ranks = ranks;
+  h->groups = groups;
+  h->g = ranks / groups;
+  // group k = ranks [k g, (k + 1) g): a limb plan of g ranks over the group's ciphertexts
+  h->group = rank / h->g;
+  h->shard = rank % h->g;
+  const u32 cb = (batch + groups - 1) / groups;
+  h->batch0 = std::min(batch, h->group * cb);
+  h->batch = std::min(batch, h->batch0 + cb) - h->batch0;
+  return fhe_dist_plan_make(&h->plan, L, log_n, h->g, h->shard, h->batch, chunks);
+}
+
+size_t fhe_keyswitch_dist_hybrid_loopback_workspace(const fhe_ctx* ctx, uint32_t ranks,
+                                                    uint32_t groups, uint32_t batch,
+                                                    uint32_t chunks) {
+  if (!ctx || ranks == 0 || groups == 0 || ranks % groups) return 0;
+  // groups run one after another on the shared workspace: group 0 has the most ciphertexts
+  fhe_dist_hybrid h;
+  if (fhe_dist_hybrid_make(&h, ctx->L, ctx->log_n, ranks, groups, 0, batch, chunks)) return 0;
+  return fhe_keyswitch_dist_loopback_workspace(ctx, h.g, std::max(h.batch, 1u), chunks);
+}
+
+int fhe_keyswitch_dist_hybrid_loopback(const fhe_ctx* ctx, uint32_t ranks, uint32_t groups,
+                                       uint64_t* const* ks0, uint64_t* const* ks1,
+                                       const uint64_t* const* d2_own,
+                                       const uint64_t* const* evk_b,
+                                       const uint64_t* const* evk_a, uint32_t batch,
+                                       uint32_t chunks, void* ws, fhe_stream_t stream) {
+  if (!ctx || ranks == 0 || groups == 0 || ranks % groups || !ks0 || !ks1 || !d2_own || !evk_b ||
+      !evk_a) {
+    set_error("fhe_keyswitch_dist_hybrid_loopback: null argument, or groups does not divide ranks");
+    return kInvalid;
+  }
+  if (batch == 0) return kOk;
+  if (!ws) {  // one internal workspace for every group, sized once (the groups run in order)
+    int rc = ensure_ws(ctx, fhe_keyswitch_dist_hybrid_loopback_workspace(ctx, ranks, groups, batch,
+                                                                         chunks),
+                       &ws, static_cast<hipStream_t>(stream));
+    if (rc) return rc;
+  }
+  const u32 g = ranks / groups;
+  for (u32 k = 0; k < groups; ++k) {
+    fhe_dist_hybrid h;
+    if (int rc = fhe_dist_hybrid_make(&h, ctx->L, ctx->log_n, ranks, groups, k * g, batch, chunks))
+      return rc;
+    // the group's g ranks: an independent limb-sharded key-switch of its ciphertexts
+    if (int rc = fhe_keyswitch_dist_loopback(ctx, g, ks0 + k * g, ks1 + k * g, d2_own + k * g,
+                                             evk_b + k * g, evk_a + k * g, h.batch, chunks, ws,
+                                             stream))
+      return rc;
+  }
   return kOk;
 }
 

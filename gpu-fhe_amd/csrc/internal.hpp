@@ -80,11 +80,10 @@ struct fhe_ctx {
   // Digit j covers Q-limbs [j * alpha, min(L, (j + 1) * alpha)).
   ulonglong2* d_modup_inv = nullptr;    // [dnum][alpha]        (D^_k)^-1 mod q_k
   ulonglong2* d_modup_hat = nullptr;    // [dnum][alpha][L + K] D^_k mod t  (by ctx limb t)
-  // the same with .y = D^_k 2^128 mod t: the fused lz16 ModUp's Montgomery conversion then emits
-  // the extended rows times R = 2^64, so k_ks_row_inner's inner product reduces by one REDC
-  ulonglong2* d_modup_hat_r = nullptr;  // [dnum][alpha][L + K]
   // the fused conversions' tables (ntt.hip k_modup_col): {h, h w0 mod t} with h the .y word of
-  // d_modup_hat (_w), d_modup_hat_r (_rw), d_moddown_hat (_w) and w0 = psi_t^(N/2), the twiddle of
+  // d_modup_hat (_w), of its Montgomery-scaled form D^_k 2^128 mod t (_rw: the fused lz16 ModUp
+  // then emits the extended rows times R = 2^64, so k_ks_row_inner's inner product reduces by one
+  // REDC; built on the host only), of d_moddown_hat (_w), and w0 = psi_t^(N/2), the twiddle of
   // the column-forward pass's stage 0, folded in for the rows that stage multiplies
   ulonglong2* d_modup_hat_w = nullptr;    // [dnum][alpha][L + K]
   ulonglong2* d_modup_hat_rw = nullptr;   // [dnum][alpha][L + K]
@@ -153,7 +152,7 @@ struct KsRowArgs {
   const u64* evk_b;
   const u64* evk_a;
   u32 rows, nq, base0, base1, alpha, L, batch;
-  // ext rows carry a factor R = 2^64 (the fused lz16 ModUp with d_modup_hat_r): the inner product
+  // ext rows carry a factor R = 2^64 (the fused lz16 ModUp with d_modup_hat_rw): the inner product
   // takes the own digit's d2 rows times R as well and reduces each 128-bit sum by one Montgomery
   // REDC (R^-1) instead of reduce128
   bool mont = false;
@@ -239,9 +238,6 @@ struct ModDownRowArgs {
   // 1: one set of polys (ks0 only, conv [batch][nq][N]), as the NTT-form rescale uses it
   u32 halves = 2;
   const ulonglong2* pinv = nullptr;  // per-limb Shoup pairs of the divisor's inverse; null: P^-1
-  // the accumulators' Q rows and conv already carry P^-1 (rns.hip pscale): the finish is
-  // acc - NTT(conv) mod q, no product
-  u32 prescaled = 0;
 };
 int launch_moddown_row(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t s);
 // NTT-form rescale, spread + column-forward pass in one (ntt.hip, k_rescale_col): last [polys][N]
@@ -318,6 +314,32 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
                            u32 nlimbs, u32 batch, void* ws, hipStream_t s,
                            const KsEpilogue* ep = nullptr, const KsHoist* hoist = nullptr);
 size_t keyswitch_workspace_bytes(const fhe_ctx* c, u32 nlimbs, u32 batch);
+// The key-switch aliasing rule (include/fhecore.h): each output span (out_words from ks0 / ks1)
+// either is d2 itself (same start, the contiguous layout: `contiguous`, out_words == d2_words) or
+// does not overlap d2's d2_words; with contiguous outputs ks0 and ks1 must not overlap each other
+// (the epilogue layouts interleave their rows by design).  FHE_EINVAL otherwise, nothing launched.
+inline bool spans_overlap(const u64* a, u64 na, const u64* b, u64 nb) {
+  return na && nb && a < b + nb && b < a + na;
+}
+inline int ks_check_alias(const u64* ks0, const u64* ks1, const u64* d2, u64 d2_words,
+                          u64 out_words, bool contiguous, const char* who) {
+  const char* name[2] = {"ks0", "ks1"};
+  const u64* out[2] = {ks0, ks1};
+  for (int h = 0; h < 2; ++h) {
+    const bool in_place = out[h] == d2 && contiguous && out_words == d2_words;
+    if (!in_place && spans_overlap(out[h], out_words, d2, d2_words)) {
+      set_error(std::string(who) + ": " + name[h] +
+                " overlaps d2 without being d2 itself (outputs are either d2, in place, or "
+                "disjoint from it)");
+      return kInvalid;
+    }
+  }
+  if (contiguous && spans_overlap(ks0, out_words, ks1, out_words)) {
+    set_error(std::string(who) + ": ks0 and ks1 overlap");
+    return kInvalid;
+  }
+  return kOk;
+}
 // Fast basis extension between contiguous ctx limb ranges: in [S][N] over limbs [s0, s0+S),
 // out [T][N] over limbs [t0, t0+T) (ranges disjoint).
 int launch_baseconv(const fhe_ctx* c, u64* out, const u64* in, u32 s0, u32 S, u32 t0, u32 T,

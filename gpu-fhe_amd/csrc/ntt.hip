@@ -1285,9 +1285,7 @@ struct FinishView {
   u32 gal = 0;    // != 0: the addend is read through sigma_gal (hoisted rotation: sigma(c0))
   u32 rbase = 0;  // slot of add[0] within its poly
   u32 log_n = 0;
-  u32 pre = 0;    // != 0: acc and conv carry P^-1 already (ModDownRowArgs::prescaled)
   __device__ __forceinline__ u64 fin(u64 a, u64 x) const {
-    if (pre) return csub(a + q - x, q);  // kernel-argument uniform
     return csub(shoup_lazy(a + q - x, pinv.x, pinv.y, q), q);
   }
   __device__ __forceinline__ u32 gal_src(u32 i) const {
@@ -1346,7 +1344,7 @@ template <int LOGN, int H>
 __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __restrict__ ks0,
                                         u64* __restrict__ ks1, const u64* __restrict__ acc,
                                         u64 acc_ws, u32 rows, u32 nq, u32 limb0, u32 batch,
-                                        u32 items, u32 halves, u32 prescaled,
+                                        u32 items, u32 halves,
                                         const ulonglong2* __restrict__ pinv,
                                         const ulonglong2* __restrict__ tw_all,
                                         const ModParams* __restrict__ mods, KsEpilogue ep) {
@@ -1374,7 +1372,7 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
   const FinishView fo{(h ? ks1 : ks0) + (u64)b * ep.out_bs + (u64)l * N + rloc,
                       acc + (h ? acc_ws : 0) + ((u64)b * rows + l) * N + rloc,
                       add ? add + (u64)b * ep.add_bs + (u64)l * N + rloc : nullptr, lane, q,
-                      pinv[limb], ep.add_gal, (u32)rloc, (u32)LOGN, prescaled};
+                      pinv[limb], ep.add_gal, (u32)rloc, (u32)LOGN};
   // column-passed by k_modup_col (inputs below 2q) or k_ntt_col (below q)
   pass_run<G::N2, true, kFinalFwd, kWaveSync, true, H, fwd_range(2, G::N1, H), true>(
       x, fo, lv, t, tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, q, {0, 0}, {0, 0});
@@ -1391,7 +1389,7 @@ __global__ FHE_KATTR void k_moddown_row(const u64* __restrict__ conv, u64* __res
 // all digits publish to LDS slot j; then every thread combines 4 of its 16 positions for both
 // outputs: acc{0,1} = sum_j x_j * evk{b,a}[j][r] (128-bit sums of DNUM products, one reduce128).
 // Rows: r < nq -> own Q-limb base0 + r, else special limb base1 + (r - nq).
-// MONT (lz16 only): the ext rows arrive times R = 2^64 (k_modup_col with d_modup_hat_r), the own
+// MONT (lz16 only): the ext rows arrive times R = 2^64 (k_modup_col with d_modup_hat_rw), the own
 // digit's d2 rows are taken times R here (by its otherwise idle wave), and each output is one
 // subtractive REDC of the 128-bit sum (R^-1 cancels the factor) plus one subtraction, instead of
 // reduce128's two Shoup products and three subtractions.
@@ -1775,7 +1773,7 @@ __global__ FHE_KATTR void k_ks_row_fin(const u64* __restrict__ ext, u64 ext_ds,
   const u32 off = crow * G::R2 + cpos;
   auto emit = [&](u64* out, const u64* add, const u64 (&f)[CW]) {
     const FinishView fv{out + obase, nullptr, add ? add + abase : nullptr, 0, q, {0, 0},
-                        ep.add_gal, (u32)rloc, (u32)LOGN, 1u};
+                        ep.add_gal, (u32)rloc, (u32)LOGN};
     const gptr_u128 o = (gptr_u128)(out + obase + off);
 #pragma unroll
     for (int e = 0; e < CW; e += 2) o[e / 2] = fv.plus(u64x2_t{f[e], f[e + 1]}, off + e);
@@ -1867,7 +1865,18 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
     row_pass<LOGN, HD>(c, true, dst, dpstride, dst, dpstride, polys, limb0, nlimbs, s);
     prof_mark(s, "ntt_row_fwd");
   } else {
-    row_pass<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
+    // the inverse streams the same way above 1 GiB (plain outputs; the split30 form feeds the
+    // key-switch, whose passes stay below 256 MiB): 4 GiB same-box, row pass -2.8 %, column pass
+    // -4.6 % (profiles/r05_intt_stream.txt)
+    const bool stream_inv = stream && !split;
+    if (stream_inv) {
+      const u64 ir = pl * G::TILES_R;
+      k_ntt_row<LOGN, false, inv_h(HD), true, true>
+          <<<item_grid(ir), G::THR_R, 0, s>>>(src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_inv,
+                                              c->d_mods);
+    } else {
+      row_pass<LOGN, HD>(c, false, src, spstride, dst, dpstride, polys, limb0, nlimbs, s);
+    }
     prof_mark(s, "ntt_row_inv");
     const ulonglong2* nf = nfold ? nfold : c->d_nfold;
     if constexpr (HD != 2) {
@@ -1882,6 +1891,14 @@ int ntt_dispatch(const fhe_ctx* c, bool fwd, const u64* src, u64 spstride, u64* 
     } else if (split) {
       set_error("split30 INTT outputs need every modulus < 2^61");
       return kUnsupported;
+    }
+    if (stream_inv) {
+      k_ntt_col<LOGN, false, inv_h(HD), true, true>
+          <<<item_grid(ic), G::THR_C, 0, s>>>(dst, nullptr, dst, nlimbs, limb0, pd, (u32)ic,
+                                              c->d_tw_inv, nf, c->d_mods);
+      prof_mark(s, "ntt_col_inv");
+      FHE_HIP_CHECK(hipGetLastError());
+      return kOk;
     }
     k_ntt_col<LOGN, false, inv_h(HD)>
         <<<item_grid(ic),
@@ -2153,7 +2170,7 @@ int moddown_row_dispatch(const fhe_ctx* c, const ModDownRowArgs& a, hipStream_t 
   if (int rc = check_grid(item_blocks(items), G::THR_R, 1, 1, "moddown_row")) return rc;
   k_moddown_row<LOGN, HD><<<dim3((u32)((items + 7) / 8 * 8)), G::THR_R, 0, s>>>(
       a.conv, a.ks0, a.ks1, a.acc, a.acc_ws, a.rows, a.nq, a.limb0, a.batch, (u32)items, a.halves,
-      a.prescaled, a.pinv ? a.pinv : c->d_pinv, c->d_tw_fwd, c->d_mods, a.ep);
+      a.pinv ? a.pinv : c->d_pinv, c->d_tw_fwd, c->d_mods, a.ep);
   return kOk;
 }
 }  // namespace

@@ -327,7 +327,8 @@ int build_rns_tables(fhe_ctx* c) {
     std::copy(inv.begin(), inv.end(), up_inv.begin() + (size_t)j * alpha);
     std::copy(hat.begin(), hat.end(), up_hat.begin() + (size_t)j * alpha * M);
   }
-  // Montgomery-scaled copy for the fused lz16 ModUp: .y = D^_k 2^128 mod t
+  // Montgomery-scaled copy for the fused lz16 ModUp: .y = D^_k 2^128 mod t (host only: the
+  // device tables built from it are d_modup_hat_rw / _rwp below)
   std::vector<Pair64> up_hat_r(up_hat);
   for (size_t i = 0; i < up_hat.size(); ++i) {
     const u64 t = c->moduli[i % M];
@@ -388,7 +389,6 @@ int build_rns_tables(fhe_ctx* c) {
       (rc = upload(&c->d_rpinv, rpinv)))
     return rc;
   if ((rc = upload(&c->d_modup_inv, up_inv)) || (rc = upload(&c->d_modup_hat, up_hat)) ||
-      (rc = upload(&c->d_modup_hat_r, up_hat_r)) ||
       (rc = upload(&c->d_moddown_inv, dn_inv)) || (rc = upload(&c->d_moddown_hat, dn_hat)) ||
       (rc = upload(&c->d_pinv, pinv)) || (rc = upload(&c->d_nfold_down, nf_down)) ||
       (rc = upload(&c->d_nfold_up, nf_up)))
@@ -430,6 +430,17 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     return rc;
   KsEpilogue ep = epi ? *epi : KsEpilogue{};
   if (ep.out_bs == 0) ep.out_bs = (u64)nlimbs * c->n;
+  // Aliasing (fhecore.h): an output may be d2_own itself (in place: same start, the contiguous
+  // [batch][nlimbs][N] layout) or lie wholly outside it.  k_ks_row_fin writes outputs while other
+  // workgroups still read d2_own, but each thread reads the d2 words at exactly the positions it
+  // later stores, so the in-place call is race-free there (and the other finishes run after the
+  // last read of d2_own); any other overlap is refused here, before the first launch.
+  if (!(hoist && hoist->modup_only)) {
+    const u64 nw = (u64)nlimbs * c->n;
+    if (int rc = ks_check_alias(ks0, ks1, d2_own, (u64)batch * nw,
+                                (u64)(batch - 1) * ep.out_bs + nw, ep.out_bs == nw, "keyswitch"))
+      return rc;
+  }
   const u32 L = c->L, K = c->K, M = L + K, alpha = c->alpha, rows = nlimbs + K;
   const u64 n = c->n, rn = (u64)rows * n, B = batch;
   u64* ext = static_cast<u64*>(ws);          // [dnum][B][rows][N]
@@ -451,7 +462,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
   // digit's source rows; the extended rows are never written in coefficient form.
   const bool fused_up = fused && alpha <= 4;
-  // lz16 fused ModUp: the extended rows come out times R = 2^64 (d_modup_hat_r), which the fused
+  // lz16 fused ModUp: the extended rows come out times R = 2^64 (d_modup_hat_rw / _rwp), which the fused
   // row kernel's Montgomery inner product cancels (KsRowArgs::mont)
   const bool mont_ext = fused_up && c->lz16;
   if (call.scaled && !fused_up) {
@@ -545,14 +556,8 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   // workgroup (k_ks_row_fin): the row kernel covers only the special rows first, their column
   // inverse runs in place in the accumulators (the ext region stays intact for the Q rows), and
   // neither the accumulators' Q rows nor k_moddown_row's pass over them touch HBM.
-  // (not when an output overlaps d2_own: the finish kernel writes outputs while other
-  // workgroups still read d2_own)
-  const u64 out_words = (u64)(batch - 1) * ep.out_bs + (u64)nlimbs * n;
-  const u64 d2_words = (u64)batch * nlimbs * n;
-  auto overlaps = [&](const u64* o) {
-    return o < d2_own + d2_words && d2_own < o + out_words;
-  };
-  const bool qfin = pscale && row_pinv && !overlaps(ks0) && !overlaps(ks1);
+  // (outputs are d2_own itself or disjoint from it: ks_check_alias above)
+  const bool qfin = pscale && row_pinv;
   if (fused) {
     KsRowArgs ka{acc, acc_ws, ext, B * rn, d2_own, evk_b, evk_a, rows, nlimbs, limb0, L,
                  alpha, L, batch, mont_ext};
@@ -605,8 +610,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
       prof_mark(s, "ks_row_fin");
       return kOk;
     }
-    ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch, ep};
-    da.prescaled = pscale ? 1u : 0u;
+    const ModDownRowArgs da{conv, ks0, ks1, acc, acc_ws, rows, nlimbs, limb0, batch, ep};
     if ((rc = launch_moddown_row(c, da, s))) return rc;
     prof_mark(s, "moddown_row_finish");
     return kOk;

@@ -65,6 +65,10 @@ SIGNATURES = {
     "fhe_keyswitch_dist_loopback_workspace": (_sz, [_vp, _u32, _u32, _u32]),
     "fhe_keyswitch_dist_loopback": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp,
                                            _vp]),
+    "fhe_dist_hybrid_make": (_i32, [_vp, _u32, _u32, _u32, _u32, _u32, _u32, _u32]),
+    "fhe_keyswitch_dist_hybrid_loopback_workspace": (_sz, [_vp, _u32, _u32, _u32, _u32]),
+    "fhe_keyswitch_dist_hybrid_loopback": (_i32, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _u32,
+                                                  _u32, _vp, _vp]),
     "fhe_rescale_workspace": (_sz, [_vp, _u32, _u32]),
     "fhe_rescale": (_i32, [_vp, _vp, _vp, _u32, _u32, _i32, _vp, _vp]),
     "fhe_automorphism": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _i32, _vp]),
@@ -134,3 +138,10 @@ class DistPlan(ctypes.Structure):
                                     "width", "chunks", "chunk_batch")] + \
                [("block_words", _u64), ("gather_words", _u64)]
 
+
+
+class DistHybrid(ctypes.Structure):
+    """fhe_dist_hybrid (include/fhecore.h): `groups` ciphertext groups x g limb shards."""
+
+    _fields_ = [(f, _u32) for f in ("ranks", "groups", "g", "group", "shard", "batch0", "batch")] + \
+               [("plan", DistPlan)]

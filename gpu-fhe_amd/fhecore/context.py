@@ -277,9 +277,11 @@ class Context:
                   "fhe_baseconv")
         return out
 
-    def keyswitch(self, d2, evk_b, evk_a, workspace=None):
+    def keyswitch(self, d2, evk_b, evk_a, workspace=None, out=None):
         """d2 [L, N] or [batch, L, N] NTT form; evk_b/evk_a [dnum, L + K, N] NTT form (one key for the
-        whole batch) -> (ks0, ks1) shaped like d2, NTT form."""
+        whole batch) -> (ks0, ks1) shaped like d2, NTT form.
+        out = (ks0, ks1): caller-provided outputs shaped like d2 (either may be d2 itself, in place;
+        any other overlap with d2 or between them raises FheError, fhecore.h)."""
         for t, nm in ((d2, "d2"), (evk_b, "evk_b"), (evk_a, "evk_a")):
             _check_tensor(t, nm, (self.n,))
         if tuple(evk_b.shape) != (self.dnum, self.L + self.K, self.n) or evk_a.shape != evk_b.shape:
@@ -287,7 +289,11 @@ class Context:
         if d2.shape[-2] != self.L:
             raise ValueError("keyswitch: d2 must be [..., L, N]")
         batch = d2.numel() // (self.L * self.n)
-        ks0, ks1 = _empty_like(d2), _empty_like(d2)
+        if out is None:
+            ks0, ks1 = _empty_like(d2), _empty_like(d2)
+        else:
+            ks0 = _check_out(out[0], d2, d2.shape, "keyswitch: ks0")
+            ks1 = _check_out(out[1], d2, d2.shape, "keyswitch: ks1")
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
             lib.fhe_keyswitch_workspace(self._ptr, self.L,
@@ -331,14 +337,15 @@ class Context:
                                           galois_elt, int(ntt_form), _stream(x)), "fhe_automorphism")
         return out
 
-    def rotate(self, ct, galois_elt: int, rot_b, rot_a, workspace=None):
+    def rotate(self, ct, galois_elt: int, rot_b, rot_a, workspace=None, out=None):
         """ct [..., 2, L, N] NTT form -> (sigma c0 + KS0(sigma c1), KS1(sigma c1)) with the
-        key-switch key rot_b/rot_a [dnum, L + K, N] from sigma_k(s) to s."""
+        key-switch key rot_b/rot_a [dnum, L + K, N] from sigma_k(s) to s.  out: a caller-provided
+        output shaped like ct, which must not overlap ct (FheError otherwise, fhecore.h)."""
         _check_tensor(ct, "ct", (2, self.L, self.n))
         if tuple(rot_b.shape) != (self.dnum, self.L + self.K, self.n) or rot_a.shape != rot_b.shape:
             raise ValueError("rotate: key must be [dnum, L + K, N]")
         batch = ct.numel() // (2 * self.L * self.n)
-        out = _empty_like(ct)
+        out = _empty_like(ct) if out is None else _check_out(out, ct, ct.shape, "rotate: out")
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
             lib.fhe_rotate_workspace(self._ptr, lib.fhe_keyswitch_pass_batch(self._ptr, batch)))
@@ -620,6 +627,50 @@ class Context:
                                                   arr(evk_b_parts), arr(evk_a_parts), batch,
                                                   chunks, _ptr(ws), _stream(ref)),
                   "fhe_keyswitch_dist_loopback")
+        return ks0, ks1
+
+
+    def keyswitch_dist_hybrid_loopback(self, groups: int, d2_parts, evk_b_parts, evk_a_parts,
+                                       chunks: int = 0, workspace=None):
+        """The hybrid partition (fhe_dist_hybrid: `groups` ciphertext groups x g limb shards, G =
+        len(d2_parts) ranks) run on this one device (fhe_keyswitch_dist_hybrid_loopback).  Rank r
+        (group r // g, shard r % g): d2 [group batch, nlimbs, N] NTT form of its group's
+        ciphertexts and LimbShard(L, g, r % g)'s limbs (None if it owns none), evk slices
+        [dnum, nlimbs + K, N].  Returns the per-rank (ks0, ks1) lists."""
+        G = len(d2_parts)
+        if not G or groups < 1 or G % groups or len(evk_b_parts) != G or len(evk_a_parts) != G:
+            raise ValueError("keyswitch_dist_hybrid_loopback: one entry per rank, groups | ranks")
+        from .dist import LimbShard
+
+        g = G // groups
+        ks0, ks1 = [None] * G, [None] * G
+        job = 0
+        for r in range(G):
+            sh = LimbShard(self.L, g, r % g)
+            d2 = d2_parts[r]
+            if sh.nlimbs == 0 or d2 is None:
+                continue
+            _check_tensor(d2, f"d2[{r}]", (sh.nlimbs, self.n))
+            for t, nm in ((evk_b_parts[r], "evk_b"), (evk_a_parts[r], "evk_a")):
+                _check_tensor(t, f"{nm}[{r}]", (self.dnum, sh.nlimbs + self.K, self.n))
+            for t, nm in ((d2, "d2"), (evk_b_parts[r], "evk_b"), (evk_a_parts[r], "evk_a")):
+                if t.device != self._dev():
+                    raise ValueError(f"keyswitch_dist_hybrid_loopback: {nm}[{r}] is on "
+                                     f"{t.device}, the context on {self._dev()}")
+            if r % g == 0:
+                job += d2.numel() // (sh.nlimbs * self.n)
+            ks0[r], ks1[r] = _empty_like(d2), _empty_like(d2)
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_keyswitch_dist_hybrid_loopback_workspace(self._ptr, G, groups, job, chunks))
+        arr = lambda ts: (ctypes.c_void_p * G)(*[t.data_ptr() if t is not None else None  # noqa: E731
+                                                  for t in ts])
+        ref = next(t for t in d2_parts if t is not None)
+        with torch.cuda.device(self.device):
+            check(lib.fhe_keyswitch_dist_hybrid_loopback(
+                self._ptr, G, groups, arr(ks0), arr(ks1), arr(d2_parts), arr(evk_b_parts),
+                arr(evk_a_parts), job, chunks, _ptr(ws), _stream(ref)),
+                "fhe_keyswitch_dist_hybrid_loopback")
         return ks0, ks1
 
 

@@ -87,6 +87,38 @@ def dist_plan(L: int, log_n: int, ranks: int, rank: int, batch: int, chunks: int
     return p
 
 
+def hybrid_plan(L: int, log_n: int, ranks: int, groups: int, rank: int, batch: int,
+                chunks: int = 0):
+    """The hybrid partition (fhe_dist_hybrid_make; host only): rank `rank` of `ranks` is limb shard
+    rank % g of ciphertext group rank // g (g = ranks / groups), which key-switches the job's
+    ciphertexts [batch0, batch0 + batch) among its g ranks (``plan``: its limb plan)."""
+    from ._capi import DistHybrid, check, load
+
+    h = DistHybrid()
+    check(load().fhe_dist_hybrid_make(ctypes.byref(h), L, log_n, ranks, groups, rank, batch,
+                                      chunks), "fhe_dist_hybrid_make")
+    return h
+
+
+def hybrid_groups(world: int, groups: int):
+    """torch.distributed sub-groups of the hybrid partition: ranks [k g, (k + 1) g) for each
+    ciphertext group k (every rank must call this, in the same order); returns this rank's group
+    (None at world 1 or groups == world, where a group is one rank)."""
+    if groups < 1 or world % groups:
+        raise ValueError(f"{groups} ciphertext groups do not divide {world} ranks")
+    g = world // groups
+    if world == 1 or g == 1:
+        return None
+    mine = None
+    me = dist.get_rank()
+    for k in range(groups):
+        ranks = list(range(k * g, (k + 1) * g))
+        grp = dist.new_group(ranks=ranks)
+        if me in ranks:
+            mine = grp
+    return mine
+
+
 def gather_ranked(x_own, shard: LimbShard, group=None):
     """[..., nlimbs, N] per rank -> [world, batch, width, N] on every rank (batch = the flattened
     leading dims; blocks shorter than `width` padded): one all_gather_into_tensor, no reorder."""
@@ -151,11 +183,13 @@ class RcclComm:
     makes the unique id; torch.distributed (any backend) carries it to the others.  One per
     process/GPU; every rank of `group` must construct it together."""
 
-    def __init__(self, device: int = None, group=None):
+    def __init__(self, device: int = None, group=None, local: bool = False):
+        """local: a one-rank communicator whatever the process group (a hybrid partition's
+        ciphertext group of one rank, fhe_dist_hybrid with g = 1)."""
         from ._capi import check, load
 
         lib = load()
-        if dist.is_available() and dist.is_initialized():
+        if dist.is_available() and dist.is_initialized() and not local:
             self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
         else:
             self.world, self.rank = 1, 0

@@ -141,7 +141,12 @@ int fhe_baseconv(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t
  * sharded outputs of G ranks concatenate to the single-device result bit for bit.
  * fhe_keyswitch (and fhe_mul_relin, fhe_rotate) run the batch in passes of at most 256 MiB of
  * d2 (the Infinity Cache), so the internal workspace is sized for one pass; a caller's workspace
- * of the documented *_workspace(ctx, ..., batch) bytes is always large enough. */
+ * of the documented *_workspace(ctx, ..., batch) bytes is always large enough.
+ * Aliasing (every key-switch entry point, incl. the _shard, _dist and _loopback forms): ks0 and
+ * ks1 may each be d2 (d2_own) itself -- the in-place call, same start pointer -- or must not
+ * overlap it at all; ks0 and ks1 must not overlap each other.  Any other overlap returns
+ * FHE_EINVAL before anything is launched.  c_all / c_gathered, the keys and the workspace must
+ * not overlap the outputs (not checked). */
 size_t fhe_keyswitch_workspace(const fhe_ctx* ctx, uint32_t nlimbs, uint32_t batch);
 /* The pass size of fhe_keyswitch / fhe_rotate / fhe_mul_relin for `batch` ciphertexts:
  * min(batch, the ciphertexts whose L limbs fit 256 MiB), at least 1 (0 for batch 0).  A workspace
@@ -226,6 +231,39 @@ int fhe_keyswitch_dist_loopback(const fhe_ctx* ctx, uint32_t ranks, uint64_t* co
                                 uint32_t batch, uint32_t chunks, void* workspace,
                                 fhe_stream_t stream);
 
+/* Hybrid partition of a key-switch batch over `ranks` GPUs: `groups` ciphertext groups of
+ * g = ranks / groups limb shards each (groups | ranks).  Rank r is limb shard r % g of group r / g;
+ * group k takes the job's ciphertexts [batch0, batch0 + batch) (contiguous, ceil(job batch /
+ * groups) per group, the last ones possibly shorter or empty) and runs the limb-sharded
+ * key-switch above among its own g ranks: `plan` is fhe_dist_plan_make(L, log_n, g, r % g, batch,
+ * chunks), the all-gather stays inside the group (the caller creates one communicator per group,
+ * g ranks, with fhe_comm_create), and per-rank work is ~ batch (L / g + K) instead of the
+ * limb-only job batch (L / ranks + K).  groups = 1 is the limb-only partition (the default);
+ * groups = ranks replicates nothing but the key: each GPU key-switches whole ciphertexts, no
+ * collective.  Host only, callable without a GPU. */
+typedef struct fhe_dist_hybrid {
+  uint32_t ranks, groups, g;
+  uint32_t group, shard;   /* rank / g, rank % g */
+  uint32_t batch0, batch;  /* the group's ciphertexts within the job's batch */
+  fhe_dist_plan plan;      /* the group's limb plan for this rank */
+} fhe_dist_hybrid;
+int fhe_dist_hybrid_make(fhe_dist_hybrid* h, uint32_t L, uint32_t log_n, uint32_t ranks,
+                         uint32_t groups, uint32_t rank, uint32_t batch, uint32_t chunks);
+/* The hybrid partition's ranks run one after another on this device (per group: the loopback
+ * above over its g ranks and its ciphertexts).  Per-rank host arrays of device pointers, rank r's
+ * d2_own / ks0 / ks1 being [group batch][nlimbs_r][N] of its group's ciphertexts and its limbs;
+ * `batch` is the job's.  The per-rank outputs equal fhe_keyswitch's rows (group k's ciphertexts,
+ * shard s's limbs) bit for bit. */
+size_t fhe_keyswitch_dist_hybrid_loopback_workspace(const fhe_ctx* ctx, uint32_t ranks,
+                                                    uint32_t groups, uint32_t batch,
+                                                    uint32_t chunks);
+int fhe_keyswitch_dist_hybrid_loopback(const fhe_ctx* ctx, uint32_t ranks, uint32_t groups,
+                                       uint64_t* const* ks0, uint64_t* const* ks1,
+                                       const uint64_t* const* d2_own,
+                                       const uint64_t* const* evk_b,
+                                       const uint64_t* const* evk_a, uint32_t batch,
+                                       uint32_t chunks, void* workspace, fhe_stream_t stream);
+
 /* ---- rescale and rotation (not in the reference) ---------------------
  * Standard RNS-CKKS operations on this library's layout, restated by oracle/pyoracle.py
  * (rescale_coeff / rescale_ntt, automorphism_*, rotate).
@@ -243,7 +281,8 @@ int fhe_rescale(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t 
 int fhe_automorphism(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t polys,
                      uint32_t limb0, uint32_t nlimbs, uint32_t galois_elt, int ntt_form,
                      fhe_stream_t stream);
-/* fhe_rotate: in, out [batch][2][L][N] NTT form over Q (out must not alias in);
+/* fhe_rotate: in, out [batch][2][L][N] NTT form over Q (out must not overlap in at all:
+ * FHE_EINVAL -- the finish reads c0 through sigma while other workgroups write out);
  * out = (sigma_k c0 + KS0(sigma_k c1), KS1(sigma_k c1)) with rot_b, rot_a [dnum][L + K][N] the
  * key-switch key from sigma_k(s) to s (NTT form, as for fhe_keyswitch). */
 size_t fhe_rotate_workspace(const fhe_ctx* ctx, uint32_t batch);

@@ -167,3 +167,52 @@ def test_single_rank_shard_is_identity():
     for i in range(2):
         r0, r1 = coracle.keyswitch(d2[i], eb, ea, qs, ps, DNUM)
         assert (_a(k0)[i] == r0).all() and (_a(k1)[i] == r1).all()
+
+
+def _hybrid_worker(rank, world, groups, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fhecore.dist import hybrid_groups, hybrid_plan
+
+        qs, ps, d2, eb, ea, _, _ = _data(seed=3)
+        B = d2.shape[0]
+        grp = hybrid_groups(world, groups)  # every rank creates every group's sub-group
+        h = hybrid_plan(L, LOG_N, world, groups, rank, B, 1)
+        shard = LimbShard(L, h.g, h.shard)
+        assert shard.world == (dist.get_world_size(grp) if grp is not None else 1)
+        eng = CpuEngine(qs, ps)
+        rows = shard.evk_rows(K)
+        mine = d2[h.batch0:h.batch0 + h.batch, shard.lo:shard.hi]
+        k0, k1 = sharded_keyswitch(eng, _t(mine), _t(eb[:, rows]), _t(ea[:, rows]), shard,
+                                   group=grp)
+        q.put((rank, h.batch0, h.batch, shard.lo, shard.hi, _a(k0).copy(), _a(k1).copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,groups", [(4, 2), (2, 2)])
+def test_hybrid_partition_gloo(world, groups):
+    """The hybrid partition's torch.distributed form (fhe_dist_hybrid): `groups`
+    ciphertext groups of world / groups limb shards, the all-gather inside each group's
+    sub-group only; every rank's rows equal the oracle key-switch of its group's ciphertexts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hybrid_worker, args=(r, world, groups, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    qs, ps, d2, eb, ea, _, _ = _data(seed=3)
+    refs = [coracle.keyswitch(d2[i], eb, ea, qs, ps, DNUM) for i in range(d2.shape[0])]
+    covered = np.zeros((d2.shape[0], L), dtype=int)
+    for _ in range(world):
+        rank, b0, bn, lo, hi, k0, k1 = q.get()
+        for i in range(bn):
+            assert (k0[i] == refs[b0 + i][0][lo:hi]).all(), (rank, i)
+            assert (k1[i] == refs[b0 + i][1][lo:hi]).all(), (rank, i)
+            covered[b0 + i, lo:hi] += 1
+    assert (covered == 1).all()

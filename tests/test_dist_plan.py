@@ -107,3 +107,41 @@ def test_bench_default_plans():
         p = dist_plan(16, 16, G, G - 1, 16, chunks)
         assert (p.nlimbs, p.chunks, p.chunk_batch) == (16 // G, chunks, 16 // chunks)
         assert p.block_words * 8 == 16 // chunks * (16 // G) * 8 << 16
+
+
+@pytest.mark.parametrize("G", range(1, 9))
+@pytest.mark.parametrize("L", [1, 7, 16, 17])
+def test_hybrid_partition_plan(G, L):
+    """fhe_dist_hybrid_make for every divisor `groups` of G: rank r is limb shard r % g of group
+    r // g; the groups' ciphertext ranges partition the job's batch in rank order; each rank's plan
+    is exactly the limb plan of its group (g ranks, its ciphertexts); within a group the shards
+    cover every limb once.  Bad shapes (groups not dividing G, rank out of range) are refused."""
+    from fhecore.dist import hybrid_plan
+
+    lib = _capi.load()
+    for groups in [d for d in range(1, G + 1) if G % d == 0]:
+        g = G // groups
+        for batch, chunks in itertools.product([0, 1, 3, 5, 16, 32], [0, 1, 4]):
+            hs = [hybrid_plan(L, LOG_N, G, groups, r, batch, chunks) for r in range(G)]
+            start = 0
+            for k in range(groups):
+                grp = hs[k * g:(k + 1) * g]
+                assert {(h.batch0, h.batch) for h in grp} == {(grp[0].batch0, grp[0].batch)}
+                assert grp[0].batch0 == min(start, batch)
+                start = grp[0].batch0 + grp[0].batch
+                lo = 0
+                for s, h in enumerate(grp):
+                    assert (h.ranks, h.groups, h.g, h.group, h.shard) == (G, groups, g, k, s)
+                    ref = dist_plan(L, LOG_N, g, s, h.batch, chunks)
+                    for f, _ in _capi.DistPlan._fields_:
+                        assert getattr(h.plan, f) == getattr(ref, f), f
+                    assert h.plan.limb0 == lo or h.plan.nlimbs == 0
+                    lo += h.plan.nlimbs
+                assert lo == L
+            assert start == batch
+    bad = _capi.DistHybrid()
+    for args in ((G, G + 1, 0), (G, 0, 0), (G, 1, G)):
+        if args[1] and G % args[1] == 0 and args[2] < G:
+            continue
+        assert lib.fhe_dist_hybrid_make(ctypes.byref(bad), L, LOG_N, args[0], args[1], args[2],
+                                        4, 0) == -1

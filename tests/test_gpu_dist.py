@@ -195,3 +195,49 @@ def test_bench_default_line_end_to_end():
     assert line["roofline"]["kernel"] == "hm_row_tensor" and line["roofline"]["frac"] > 0
     assert line["keyswitch_leg"]["value"] > 0
     assert line["dist_check"]["result"] == "bit-exact"
+
+
+@pytest.mark.parametrize("log_n,G,groups,batch,chunks", [
+    (16, 8, 4, 8, 2),   # g = 2 limb shards x 4 ciphertext groups (configs[3] key shape)
+    (16, 8, 2, 6, 0),   # g = 4 x 2 groups, default chunking
+    (16, 8, 8, 8, 1),   # g = 1: every rank key-switches whole ciphertexts, no gather
+    (12, 8, 4, 5, 2),   # uneven groups: 2, 2, 1, 0 ciphertexts
+    (12, 6, 2, 7, 4),   # g = 3: uneven shards 6, 6, 4 of L = 16
+])
+def test_keyswitch_dist_hybrid_loopback(fc, log_n, G, groups, batch, chunks):
+    """The hybrid partition (fhe_dist_hybrid: `groups` ciphertext groups x g = G / groups limb
+    shards, the all-gather inside each group) executed for all G virtual ranks on this GPU: rank r's
+    outputs are fhe_keyswitch's rows of its group's ciphertexts and its shard's limbs, bit for bit
+    (DESIGN.md §7 models its rates)."""
+    from fhecore.dist import LimbShard, hybrid_plan
+
+    L, K, dnum = 16, 4, 4
+    ctx = fc.Context(log_n, L=L, K=K, dnum=dnum)
+    d2 = rand(ctx.moduli, log_n, (batch,), seed=31 + G * groups)
+    eb = rand(ctx.all_moduli, log_n, (dnum,), seed=32)
+    ea = rand(ctx.all_moduli, log_n, (dnum,), seed=33)
+    full0, full1 = (fc.to_host(t) for t in ctx.keyswitch(fc.to_device(d2), fc.to_device(eb),
+                                                          fc.to_device(ea)))
+    g = G // groups
+    plans = [hybrid_plan(L, log_n, G, groups, r, batch, chunks) for r in range(G)]
+    d2p, ebp, eap = [], [], []
+    for r, h in enumerate(plans):
+        assert (h.g, h.group, h.shard) == (g, r // g, r % g)
+        sh = LimbShard(L, g, h.shard)
+        assert (h.plan.limb0, h.plan.nlimbs, h.plan.batch) == (sh.lo, sh.nlimbs, h.batch)
+        rows = sh.evk_rows(K)
+        d2p.append(fc.to_device(np.ascontiguousarray(d2[h.batch0:h.batch0 + h.batch, sh.lo:sh.hi]))
+                   if sh.nlimbs else None)
+        ebp.append(fc.to_device(np.ascontiguousarray(eb[:, rows])) if sh.nlimbs else None)
+        eap.append(fc.to_device(np.ascontiguousarray(ea[:, rows])) if sh.nlimbs else None)
+    ks0, ks1 = ctx.keyswitch_dist_hybrid_loopback(groups, d2p, ebp, eap, chunks=chunks)
+    covered = np.zeros((batch, L), dtype=int)
+    for r, h in enumerate(plans):
+        if ks0[r] is None:
+            continue
+        sh = LimbShard(L, g, h.shard)
+        sl = (slice(h.batch0, h.batch0 + h.batch), slice(sh.lo, sh.hi))
+        assert (fc.to_host(ks0[r]) == full0[sl]).all(), r
+        assert (fc.to_host(ks1[r]) == full1[sl]).all(), r
+        covered[sl] += 1
+    assert (covered == 1).all()  # every (ciphertext, limb) row exactly once

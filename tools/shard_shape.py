@@ -81,12 +81,79 @@ def ks_partition_model(out, L, K, B, n):
     return res
 
 
+def hybrid_shapes(gen, B, warmup=20, steps=50):
+    """Per-rank compute of the hybrid partition's key-switch leg (fhe_dist_hybrid: G / g ciphertext
+    groups x g limb shards) at G = 2, 4, 8 for every divisor g, timed on this GPU, plus the xGMI
+    model of the group's all-gather.  Rank 0 of group 0 (the fullest group: ceil(B g / G)
+    ciphertexts, the widest shard) runs its chunked local step exactly as fhe_keyswitch_dist does
+    after each gather: 4 chunks when g > 1, one call and no gather when g = 1."""
+    Lk, K, dnum, log_n = 16, 4, 4, 16
+    n = 1 << log_n
+    lib = load()
+    ctx = fc.Context(log_n, L=Lk, K=K, dnum=dnum)
+    res = {"assumptions": {"link_GBps_per_direction": LINK_GBPS_DIR, "batch": B,
+                           "comm": "each rank receives (g - 1) peer blocks of its group's chunk; "
+                                   "direct: one link per peer at the per-direction peak; ring: "
+                                   "0.7 x (g - 1) links' aggregate",
+                           "step": "first chunk's gather exposed + max(compute, the other chunks' "
+                                   "gathers), the chunked overlap of fhe_keyswitch_dist"}}
+    for G in (1, 2, 4, 8):
+        for g in [d for d in (1, 2, 4, 8) if d <= G and G % d == 0]:
+            groups = G // g
+            sh = fdist.LimbShard(Lk, g, 0)
+            gb = -(-B // groups)  # group 0's ciphertexts
+            c = 1 if g == 1 else min(4, gb)
+            cb = -(-gb // c)
+            rows = sh.evk_rows(K)
+            allm = ctx.all_moduli
+            eb = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
+            ea = uniform_limbs(gen, [allm[r] for r in rows], (dnum,), n)
+            d2 = uniform_limbs(gen, ctx.moduli[sh.lo:sh.hi], (cb,), n)
+            gat = torch.zeros(g * cb * sh.width * n, dtype=torch.int64, device="cuda")
+            ks0 = ctx.empty(cb, sh.nlimbs, n)
+            ks1 = ctx.empty(cb, sh.nlimbs, n)
+            ws = ctx.workspace(lib.fhe_keyswitch_workspace(ctx.handle, sh.nlimbs, cb))
+
+            def chunked():
+                for _ in range(c):
+                    ctx.intt(d2, limb0=sh.lo)
+                    rc = lib.fhe_keyswitch_shard_ranked(
+                        ctx.handle, ks0.data_ptr(), ks1.data_ptr(), gat.data_ptr(), g,
+                        d2.data_ptr(), eb.data_ptr(), ea.data_ptr(), sh.lo, sh.nlimbs, cb,
+                        ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                    assert rc == 0, lib.fhe_last_error()
+
+            comp = rate(chunked, warmup, steps) * 1e3
+            peer = gb * sh.width * n * 8  # one peer's block of the group's whole gather
+            recv = (g - 1) * peer
+            direct = peer / (LINK_GBPS_DIR * 1e9) * 1e3 if g > 1 else 0.0
+            ring = recv / (0.7 * (g - 1) * LINK_GBPS_DIR * 1e9) * 1e3 if g > 1 else 0.0
+            ent = {"groups": groups, "limb_shards_g": g, "limbs_per_gpu": sh.nlimbs,
+                   "ciphertexts_per_group": gb, "chunks": c, "compute_ms": round(comp, 4),
+                   "recv_MB": round(recv / 1e6, 1)}
+            for tag, cm in (("direct", direct), ("ring", ring)):
+                step = cm / c + max(comp, cm * (c - 1) / c)
+                ent[f"step_ms_{tag}"] = round(step, 4)
+                ent[f"keyswitch_per_s_{tag}"] = round(B / step * 1e3, 1)
+            res[f"G={G} g={g}"] = ent
+            del eb, ea, d2, gat, ks0, ks1, ws
+            torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--ks-batch", type=int, default=32, help="the key-switch leg's batch (bench.py)")
+    ap.add_argument("--hybrid", action="store_true",
+                    help="only the hybrid partition's rank shapes and model (fhe_dist_hybrid)")
     args = ap.parse_args()
+    if args.hybrid:
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(6)
+        print(json.dumps({"ks hybrid partition": hybrid_shapes(gen, args.ks_batch)}, indent=1))
+        return
     log_n, n, L = 16, 1 << 16, 8
     ctx = fc.Context(log_n, L=L)
     gen = torch.Generator(device="cuda")
