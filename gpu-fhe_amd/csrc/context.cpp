@@ -93,17 +93,25 @@ int ctx_create(fhe_ctx** out, u32 log_n, const u64* q, u32 L, const u64* p, u32 
   c->moduli = mods;
   const size_t M = mods.size();
   std::vector<Pair64> twf(M * n), twi(M * n), nfold(4 * M);
+  // the HomMult's 9 + 7-stage forward (ntt.hip k_hm_col9) needs its own row layout of the forward
+  // table: narrow contexts at N = 2^16 (Q limbs only: HomMult never runs on P limbs)
+  const bool split9 = log_n == 16 && !c->wide;
+  std::vector<Pair64> twf9(split9 ? L * n : 0);
   c->psi.resize(M);
   c->mods_host.resize(M);
   for (size_t i = 0; i < M; ++i) {
     c->mods_host[i] = make_mod_params(mods[i]);
-    c->psi[i] = ntt_tables(mods[i], log_n, &twf[i * n], &twi[i * n], &nfold[4 * i]);
+    c->psi[i] = ntt_tables(mods[i], log_n, &twf[i * n], &twi[i * n], &nfold[4 * i],
+                           split9 && i < L ? &twf9[i * n] : nullptr);
   }
   int rc = kOk;
   if ((rc = upload(&c->d_mods, c->mods_host.data(), M)) ||
       (rc = upload(&c->d_tw_fwd, reinterpret_cast<const ulonglong2*>(twf.data()), M * n)) ||
       (rc = upload(&c->d_tw_inv, reinterpret_cast<const ulonglong2*>(twi.data()), M * n)) ||
-      (rc = upload(&c->d_nfold, reinterpret_cast<const ulonglong2*>(nfold.data()), 4 * M)) || (rc = build_rns_tables(c)) ||
+      (rc = upload(&c->d_nfold, reinterpret_cast<const ulonglong2*>(nfold.data()), 4 * M)) ||
+      (split9 && (rc = upload(&c->d_tw_fwd9, reinterpret_cast<const ulonglong2*>(twf9.data()),
+                              (size_t)L * n))) ||
+      (rc = build_rns_tables(c)) ||
       (rc = build_galois_tables(c))) {
     ctx_destroy(c);
     return rc;
@@ -116,7 +124,7 @@ int ctx_destroy(fhe_ctx* c) {
   if (!c) return kOk;
   (void)hipSetDevice(c->device);
   for (auto& t : c->bc_tables) (void)hipFree(t.second);
-  for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_inv, (void*)c->d_nfold, (void*)c->d_nfold_down, (void*)c->d_nfold_up,
+  for (void* ptr : {(void*)c->d_mods, (void*)c->d_tw_fwd, (void*)c->d_tw_fwd9, (void*)c->d_tw_inv, (void*)c->d_nfold, (void*)c->d_nfold_down, (void*)c->d_nfold_up,
                     (void*)c->d_modup_inv, (void*)c->d_modup_hat, (void*)c->d_moddown_inv,
                     (void*)c->d_moddown_hat, (void*)c->d_modup_hat_w, (void*)c->d_modup_hat_rw,
                     (void*)c->d_moddown_hat_w, (void*)c->d_modup_hat_rwp,

@@ -152,11 +152,12 @@ bool gen_moduli_host(u32 log_n, u32 count, u32 bits, u32 skip, u64* out, std::st
 // g = t W + sj, W = 2^(elog - b - 1), sj < W.  Those stages' segments [(R1 + r) 2^st, +2^st) of
 // every limb's table are stored transposed -- entry g at sj TPS + t, TPS = R2 / 2^elog -- so one
 // twiddle load instruction reads consecutive words across the wavefront's lanes.
-void lane_major_rows(Pair64* tw, size_t entries, u32 log_n, int elog) {
+void lane_major_rows(Pair64* tw, size_t entries, u32 log_n, int elog, int n1, int kb_last) {
   const u32 n = 1u << log_n;
-  const int n1 = (int)log_n / 2, n2 = (int)log_n - n1;
+  if (n1 < 0) n1 = (int)log_n / 2;
+  const int n2 = (int)log_n - n1;
   const int nr = (n2 + elog - 1) / elog;
-  const int kb_last = n2 / nr + (nr - 1 < n2 % nr ? 1 : 0);
+  if (kb_last < 0) kb_last = n2 / nr + (nr - 1 < n2 % nr ? 1 : 0);
   const u32 r1 = 1u << n1, tps = 1u << (n2 - elog);
   std::vector<Pair64> seg;
   for (size_t base = 0; base + n <= entries; base += n)
@@ -171,7 +172,7 @@ void lane_major_rows(Pair64* tw, size_t entries, u32 log_n, int elog) {
     }
 }
 
-u64 ntt_tables(u64 q, u32 log_n, Pair64* twf, Pair64* twi, Pair64* nfold) {
+u64 ntt_tables(u64 q, u32 log_n, Pair64* twf, Pair64* twi, Pair64* nfold, Pair64* twf9) {
   const u64 n = 1ull << log_n;
   const u64 psi = find_psi(q, log_n), psi_inv = powmod_u64(psi, q - 2, q);
   std::vector<u64> pw(n), pwi(n);
@@ -192,6 +193,10 @@ u64 ntt_tables(u64 q, u32 log_n, Pair64* twf, Pair64* twi, Pair64* nfold) {
   nfold[1] = shoup_pair(nf1, q);
   nfold[2] = shoup_pair(mulmod_u64(n_inv, r_mod, q), q);  // HomMult: undo the tensor's R^-1
   nfold[3] = shoup_pair(mulmod_u64(nf1, r_mod, q), q);
+  if (twf9) {  // the 512 x 128 split's forward rows (HomMult at N = 2^16: k_hm_col9 + 7-stage rows)
+    std::copy(twf, twf + n, twf9);
+    lane_major_rows(twf9, n, log_n, 4, (int)log_n / 2 + 1, 4);  // rounds 3 + 4 (SMALL_FIRST)
+  }
   lane_major_rows(twf, n, log_n, 4);
   lane_major_rows(twi, n, log_n, 4);
   return psi;

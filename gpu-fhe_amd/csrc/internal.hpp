@@ -67,6 +67,9 @@ struct fhe_ctx {
   fhe::ModParams* d_mods = nullptr;  // [L + K]
   ulonglong2* d_tw_fwd = nullptr;    // [L + K][N] (psi^brv(k), Shoup)
   ulonglong2* d_tw_inv = nullptr;    // [L + K][N] (psi^-brv(k), Shoup)
+  // [L][N] the forward table with the row layout of the 512 x 128 split (N = 2^16, narrow
+  // contexts; the HomMult's 7-stage forward rows after k_hm_col9), else null
+  ulonglong2* d_tw_fwd9 = nullptr;
   // (both tables: the row-pass stages of the low-bit round are stored lane-major, context.cpp
   // lane_major_rows)
   // [L + K][4] Shoup pairs: N^-1, psi^-1 N^-1 (last inverse stage), and the same times

@@ -67,11 +67,15 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// Round split of a 2^LOGR-point sub-transform into NR rounds of <= kElog stages.
-template <int LOGR>
+// Round split of a 2^LOGR-point sub-transform into NR rounds of <= 2^EL-point stages; the longer
+// rounds come first, or last with SMALL_FIRST (the HomMult's 7-stage forward rows: 3 + 4, so the
+// first round's loads and the last round's low bits are whole 16-byte pairs / 16-element runs).
+template <int LOGR, int EL = kElog, bool SMALL_FIRST = false>
 struct Rounds {
-  static constexpr int NR = (LOGR + kElog - 1) / kElog;
-  static constexpr int kb(int k) { return LOGR / NR + (k < LOGR % NR ? 1 : 0); }
+  static constexpr int NR = (LOGR + EL - 1) / EL;
+  static constexpr int kb(int k) {
+    return LOGR / NR + ((SMALL_FIRST ? NR - 1 - k : k) < LOGR % NR ? 1 : 0);
+  }
   // bit positions covered by round k: forward rounds go top-down, inverse bottom-up
   static constexpr int lo_fwd(int k) {
     int hi = LOGR;
@@ -86,9 +90,10 @@ struct Rounds {
 // Which position bits of the sub-transform a thread's element index j owns in one round:
 // bits [LO, LO + KB) are butterflied; the remaining kElog - KB bits of j take the lowest free
 // positions; the thread index fills every other bit, ascending.
-template <int LOGR, int KB, int LO>
+template <int LOGR, int KB, int LO, int EL = kElog>
 struct Layout {
-  static constexpr int E = kE;
+  static constexpr int EB = EL;  // log2 of the elements per thread
+  static constexpr int E = 1 << EL;
   static constexpr int ex_pos(int k) {
     int found = 0;
     for (int i = 0; i < LOGR; ++i) {
@@ -102,11 +107,14 @@ struct Layout {
     u32 p = 0;
     for (int b = 0; b < KB; ++b)
       if ((j >> b) & 1) p |= 1u << (LO + b);
-    for (int b = 0; b < kElog - KB; ++b)
+    for (int b = 0; b < EL - KB; ++b)
       if ((j >> (KB + b)) & 1) p |= 1u << ex_pos(b);
     return p;
   }
   static constexpr u32 jmask = jpos(E - 1);
+  // every thread-index bit sits below the butterflied bits: a stage's twiddle group then depends on
+  // the element index only (wave-uniform), as in the column passes' top-bit rounds
+  static constexpr bool kTpBelow = ((jmask >> LO) + 1) == (1u << (LOGR - LO));
   static __device__ __forceinline__ u32 tpos(u32 t) {
     u32 p = 0;
     int k = 0;
@@ -188,18 +196,19 @@ static inline PolyMap flat_map(u64 pstride) { return PolyMap{1, pstride, 0, pstr
 // The distinct twiddles of one round: butterfly (stage b, pair j) uses twiddle group
 // g = (tp | jpos(j)) >> (LO + b + 1); slot[b][j] numbers the distinct (b, g - tp part) pairs and
 // rep[] keeps one representative j per slot.
-template <int LOGR, int KB, int LO>
+template <int LOGR, int KB, int LO, int EL = kElog>
 struct TwSlots {
-  using Lay = Layout<LOGR, KB, LO>;
+  using Lay = Layout<LOGR, KB, LO, EL>;
+  static constexpr int E = 1 << EL;
   struct Tab {
     int ns = 0;
-    int slot[kElog][kE] = {};
-    int rep_b[kElog * kE] = {}, rep_j[kElog * kE] = {};
+    int slot[EL][E] = {};
+    int rep_b[EL * E] = {}, rep_j[EL * E] = {};
   };
   static constexpr Tab make() {
     Tab t{};
     for (int b = 0; b < KB; ++b)
-      for (int j = 0; j < kE; ++j) {
+      for (int j = 0; j < E; ++j) {
         if (j & (1 << b)) continue;
         const u32 key = Lay::jpos(j) >> (LO + b + 1);
         int found = -1;
@@ -299,13 +308,14 @@ constexpr int gs_in(int j, int k) {
 // PRE0 (forward, k_modup_col): the operands of stage 0's products arrive already multiplied by
 // its twiddle (the base conversion folds it into its constants), so stage 0 only adds.
 template <int LOGR, int KB, int LO, bool FWD, int FIN, bool GATHER = false, int H = 8,
-          int RIN = 8, bool ROWTAB = GATHER, bool CHAIN = GATHER, bool PRE0 = false>
-__device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
+          int RIN = 8, bool ROWTAB = GATHER, bool CHAIN = GATHER, bool PRE0 = false,
+          int EL = kElog>
+__device__ __forceinline__ void round_compute(u64 (&x)[1 << EL], const u32 tp,
                                               const ulonglong2* __restrict__ tw, const u32 base,
                                               const u64 q, const ulonglong2 nf0,
                                               const ulonglong2 nf1) {
-  using Lay = Layout<LOGR, KB, LO>;
-  using TS = TwSlots<LOGR, KB, LO>;
+  using Lay = Layout<LOGR, KB, LO, EL>;
+  using TS = TwSlots<LOGR, KB, LO, EL>;
   constexpr int E = Lay::E;
   ulonglong2 tws[GATHER && TS::T.ns > 0 ? TS::T.ns : 1];
   if constexpr (GATHER) {
@@ -319,7 +329,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
         // tp = t << kElog); the row tables store those stages lane-major (host_tables.cpp
         // lane_major_rows), so the load index is sj TPS + t and a wavefront reads contiguous words
         const u32 sj = Lay::jpos(TS::T.rep_j[sl]) >> (bitpos + 1);
-        const u32 g = (ROWTAB && LO == 0) ? sj * ((1u << LOGR) / E) + (tp >> kElog)
+        const u32 g = (ROWTAB && LO == 0) ? sj * ((1u << LOGR) / E) + (tp >> EL)
                                           : (tp >> (bitpos + 1)) | sj;
         tws[sl] = ld_tw(tw + (base << st) + g);
       }
@@ -329,7 +339,9 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
   static_assert(GATHER || !(ROWTAB && LO == 0), "lane-major row twiddles are gathered");
   auto twiddle = [&](int b, int j, int bitpos, int st) {
     if constexpr (GATHER) return tws[TS::T.slot[b][j]];
-    const u32 g = (tp >> (bitpos + 1)) | (Lay::jpos(j) >> (bitpos + 1));
+    // (kTpBelow: tp >> (bitpos + 1) is 0, written out so the address is visibly uniform and the
+    // pair can come through the scalar cache into SGPRs)
+    const u32 g = (Lay::kTpBelow ? 0u : (tp >> (bitpos + 1))) | (Lay::jpos(j) >> (bitpos + 1));
     return ld_tw(tw + (base << st) + g);
   };
   const u64 q2 = 2 * q, nq = 0 - q;
@@ -524,7 +536,7 @@ __device__ __forceinline__ void round_compute(u64 (&x)[kE], const u32 tp,
 // Whether a round's kE positions are tp + 0..kE-1 (contiguous words: 16-byte accesses).
 template <class Lay>
 constexpr bool contiguous16() {
-  for (int j = 0; j < kE; ++j)
+  for (int j = 0; j < Lay::E; ++j)
     if (Lay::jpos(j) != (u32)j) return false;
   return true;
 }
@@ -561,31 +573,33 @@ struct GView {
   u64* base;
   u32 lane;
   template <class Lay>
-  __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
+  __device__ __forceinline__ void load(u64 (&x)[Lay::E], u32 tp) const {
     const u32 off = lane + tp * STRIDE;
     if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
       const gptr_u128 v = (gptr_u128)(base + off);
 #pragma unroll
-      for (int j = 0; j < kE / 2; ++j) {
+      for (int j = 0; j < Lay::E / 2; ++j) {
         const u64x2_t w = gld<NT>(v + j);
         x[2 * j] = w.x;
         x[2 * j + 1] = w.y;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) x[j] = gld<NT>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off);
+      for (int j = 0; j < Lay::E; ++j)
+        x[j] = gld<NT>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off);
     }
   }
   template <class Lay>
-  __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
+  __device__ __forceinline__ void store(const u64 (&x)[Lay::E], u32 tp) const {
     const u32 off = lane + tp * STRIDE;
     if constexpr (STRIDE == 1 && contiguous16<Lay>()) {
       const gptr_u128 v = (gptr_u128)(base + off);
 #pragma unroll
-      for (int j = 0; j < kE / 2; ++j) gst<NTS>(v + j, u64x2_t{x[2 * j], x[2 * j + 1]});
+      for (int j = 0; j < Lay::E / 2; ++j) gst<NTS>(v + j, u64x2_t{x[2 * j], x[2 * j + 1]});
     } else {
 #pragma unroll
-      for (int j = 0; j < kE; ++j) gst<NTS>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off, x[j]);
+      for (int j = 0; j < Lay::E; ++j)
+        gst<NTS>((gptr_u64)(base + (u64)Lay::jpos(j) * STRIDE) + off, x[j]);
     }
   }
   // Linear store of a row: thread t of the row's TPS threads owns positions 2 t + 2 TPS jj
@@ -621,14 +635,14 @@ struct LView {
   u64* s;
   __device__ __forceinline__ u32 idx(u32 p) const { return p * PS + (PAD16 ? (p >> 4) : 0); }
   template <class Lay>
-  __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
+  __device__ __forceinline__ void load(u64 (&x)[Lay::E], u32 tp) const {
 #pragma unroll
-    for (int j = 0; j < kE; ++j) x[j] = s[idx(tp | Lay::jpos(j))];
+    for (int j = 0; j < Lay::E; ++j) x[j] = s[idx(tp | Lay::jpos(j))];
   }
   template <class Lay>
-  __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
+  __device__ __forceinline__ void store(const u64 (&x)[Lay::E], u32 tp) const {
 #pragma unroll
-    for (int j = 0; j < kE; ++j) s[idx(tp | Lay::jpos(j))] = x[j];
+    for (int j = 0; j < Lay::E; ++j) s[idx(tp | Lay::jpos(j))] = x[j];
   }
 };
 
@@ -638,22 +652,25 @@ struct LView {
 // row takes is swapped by bit 4 of p, so both exchange patterns (p = t + 16 j and p = 16 t + j,
 // t and t + 1 in one half-wavefront) land in different halves.  32 KB per workgroup instead of
 // 34 KB with a pad column: 5 workgroups per CU instead of 4.
-template <int S>
+// SW: the position bit that picks the half-block; kElog (bit 4) for E = 16 threads.  With E = 32
+// (the 512-row HomMult column pass, k_hm_col9) the second round's threads sit 32 positions apart,
+// so the swap bit is 5 there (model-checked with the layouts, tests/test_modarith_model.py).
+template <int S, int SW = kElog>
 struct LViewC {
   u64* s;
   __device__ __forceinline__ u32 idx(u32 p) const {
     if constexpr (S >= 32) return p * S;
-    return (p >> 1) * 32 + (((p ^ (p >> 4)) & 1u) << 4);
+    return (p >> 1) * 32 + (((p ^ (p >> SW)) & 1u) << 4);
   }
   template <class Lay>
-  __device__ __forceinline__ void load(u64 (&x)[kE], u32 tp) const {
+  __device__ __forceinline__ void load(u64 (&x)[Lay::E], u32 tp) const {
 #pragma unroll
-    for (int j = 0; j < kE; ++j) x[j] = s[idx(tp | Lay::jpos(j))];
+    for (int j = 0; j < Lay::E; ++j) x[j] = s[idx(tp | Lay::jpos(j))];
   }
   template <class Lay>
-  __device__ __forceinline__ void store(const u64 (&x)[kE], u32 tp) const {
+  __device__ __forceinline__ void store(const u64 (&x)[Lay::E], u32 tp) const {
 #pragma unroll
-    for (int j = 0; j < kE; ++j) s[idx(tp | Lay::jpos(j))] = x[j];
+    for (int j = 0; j < Lay::E; ++j) s[idx(tp | Lay::jpos(j))] = x[j];
   }
 };
 
@@ -680,7 +697,9 @@ __device__ __forceinline__ u32 half_pos(u32 p) {
   return (p & ((1u << SB) - 1)) | ((p >> (SB + 1)) << SB);
 }
 template <int LOGR, class LayW, class LayR, class LV>
-__device__ __forceinline__ void half_exchange(u64 (&x)[kE], const LV& lv, u32 t) {
+__device__ __forceinline__ void half_exchange(u64 (&x)[LayW::E], const LV& lv, u32 t) {
+  constexpr int kE = LayW::E;
+  static_assert(LayR::E == kE, "one element count for both rounds");
   constexpr int SB = half_split_bit<LayW::jmask, LayR::jmask>();
   static_assert(SB >= 0 && SB < LOGR, "no element bit of the writer is a thread bit of the reader");
   constexpr u32 S = 1u << SB;
@@ -708,10 +727,11 @@ __device__ __forceinline__ void half_exchange(u64 (&x)[kE], const LV& lv, u32 t)
 }
 
 // Round-0 global load of one sub-transform into registers.
-template <int LOGR, bool FWD, class GIn>
-__device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
-  using Rd = Rounds<LOGR>;
-  using Lay = Layout<LOGR, FWD ? Rd::kb(0) : Rd::kb_inv(0), FWD ? Rd::lo_fwd(0) : Rd::lo_inv(0)>;
+template <int LOGR, bool FWD, int EL = kElog, class GIn>
+__device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[1 << EL]) {
+  using Rd = Rounds<LOGR, EL>;
+  using Lay = Layout<LOGR, FWD ? Rd::kb(0) : Rd::kb_inv(0), FWD ? Rd::lo_fwd(0) : Rd::lo_inv(0),
+                     EL>;
   gin.template load<Lay>(x, Lay::tpos(t));
 }
 
@@ -724,20 +744,22 @@ __device__ __forceinline__ void pass_load(const GIn& gin, u32 t, u64 (&x)[kE]) {
 // direct store instruction writes 16 of every 16 E bytes across 16 E * 64 bytes.
 // HALF: the column passes' one exchange (two rounds) through half the tile's LDS (half_exchange).
 template <int LOGR, bool FWD, int FIN, int SYNC, bool GATHER, int H, int R0, bool XOUT = false,
-          bool CHAIN = GATHER, bool HALF = false, bool PRE0 = false, class GOut, class LV>
-__device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const LV& lv, u32 t,
+          bool CHAIN = GATHER, bool HALF = false, bool PRE0 = false, int EL = kElog, class GOut,
+          class LV>
+__device__ __forceinline__ void pass_run(u64 (&x)[1 << EL], const GOut& gout, const LV& lv, u32 t,
                                          const ulonglong2* __restrict__ tw, u32 base, u64 q,
                                          ulonglong2 nf0, ulonglong2 nf1) {
-  using Rd = Rounds<LOGR>;
+  using Rd = Rounds<LOGR, EL>;
   static_for<0, Rd::NR>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int KB = FWD ? Rd::kb(k) : Rd::kb_inv(k);
     constexpr int LO = FWD ? Rd::lo_fwd(k) : Rd::lo_inv(k);
     constexpr int F = (k == Rd::NR - 1) ? FIN : kNotFinal;
     constexpr int RIN = fwd_range(R0, Rd::lo_fwd(0) + Rd::kb(0) - (LO + KB), H);  // stages before
-    using Lay = Layout<LOGR, KB, LO>;
+    using Lay = Layout<LOGR, KB, LO, EL>;
     const u32 tp = Lay::tpos(t);
     static_assert(!HALF || (Rd::NR == 2 && SYNC == kBlockSync), "half exchange: column, 2 rounds");
+    static_assert(!XOUT || EL == kElog, "linear row stores: 16 elements per thread");
     if constexpr (k > 0 && !HALF) {  // (HALF: half_exchange already loaded this round's layout)
       lds_sync<SYNC>();
       lv.template load<Lay>(x, tp);
@@ -747,7 +769,7 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     // column pass's few shared twiddles are left to the scheduler
     const ulonglong2* twk = tw;
     if constexpr (GATHER) asm volatile("" : "+s"(twk));
-    round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN, GATHER, CHAIN, PRE0 && k == 0>(
+    round_compute<LOGR, KB, LO, FWD, F, GATHER, H, RIN, GATHER, CHAIN, PRE0 && k == 0, EL>(
         x, tp, twk, base, q, nf0, nf1);
     if constexpr (k == Rd::NR - 1) {
       if constexpr (XOUT) {
@@ -771,7 +793,7 @@ __device__ __forceinline__ void pass_run(u64 (&x)[kE], const GOut& gout, const L
     } else if constexpr (HALF) {
       constexpr int KN = FWD ? Rd::kb(k + 1) : Rd::kb_inv(k + 1);
       constexpr int LN = FWD ? Rd::lo_fwd(k + 1) : Rd::lo_inv(k + 1);
-      half_exchange<LOGR, Lay, Layout<LOGR, KN, LN>>(x, lv, t);
+      half_exchange<LOGR, Lay, Layout<LOGR, KN, LN, EL>>(x, lv, t);
     } else {
       // the (free) wave-local fence before round 0's store keeps the row passes' LDS stores
       // together after the butterflies, which measured faster than letting them interleave
@@ -935,6 +957,55 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src, u64* __restrict
                                    rest % G::TILES_R, tw_all, mods);
 }
 
+// HomMult column forward on the 512 x 128 view of N = 2^16 (the first 9 of the 16 stages; the fused
+// row kernel then runs 7 on 128-word rows, k_hommult_row S9): 32 elements per thread in two rounds
+// of 5 + 4 stages with one exchange through half the tile (LViewC swap bit 5: both rounds' access
+// patterns conflict-free), tiles of 16 columns x 512 rows (256 threads, 16 per column), 32 KB of
+// LDS.  Moves a stage of the 4 forward polys out of the issue-bound row kernel into this
+// HBM-bound pass (the 2^9 x 2^7 split).  Same item placement and poly map as
+// k_ntt_col (a's and b's polys into the 4-slot workspace).
+constexpr int kC9Log = 9, kC9El = 5, kC9R2 = 128, kC9Subs = 16, kC9Tiles = kC9R2 / kC9Subs;
+// occupancy target: 4 waves per SIMD (104 VGPRs, no spill); 5 (96 VGPRs + 60 B of scratch)
+// measured col9 0.389 -> 0.452 ms (profiles/r06_split9_ab.txt)
+#ifndef FHE_C9_WAVES
+#define FHE_C9_WAVES 4
+#endif
+template <int H>
+__global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(FHE_C9_WAVES, 8))) void
+k_hm_col9(const u64* __restrict__ src, const u64* __restrict__ src2, u64* __restrict__ dst,
+          u32 nlimbs, u32 limb0, PolyMap pm, u32 items, const ulonglong2* __restrict__ tw_all,
+          const ModParams* __restrict__ mods) {
+  constexpr u64 N = 1ull << 16;
+  static_assert(kC9Subs * (1 << (kC9Log - kC9El)) == kColThreads, "16 threads per column");
+  __shared__ u64 lds[(1 << kC9Log) * kC9Subs / 2];
+  const u32 it = blockIdx.x;
+  if (it >= items) return;
+  u32 tile, pl;
+  if ((items / kC9Tiles) % 8 == 0) {  // XCD-grouped, as k_ntt_col
+    const u32 k = it / 8;
+    tile = k % kC9Tiles;
+    pl = (k / kC9Tiles) * 8 + it % 8;
+  } else {
+    tile = it % kC9Tiles;
+    pl = it / kC9Tiles;
+  }
+  const u32 p = pl / nlimbs, l = pl % nlimbs;
+  const u32 sub = threadIdx.x % kC9Subs, t = threadIdx.x / kC9Subs;
+  const LViewC<kC9Subs, 5> lv{lds + sub};
+  const u64 loc = (u64)l * N + (u64)tile * kC9Subs;
+  const u64* s = (pm.second(p) ? src2 + pm.src2(p) : src + pm.src(p)) + loc;
+  const u32 limb = __builtin_amdgcn_readfirstlane(limb0 + l);
+  u64 x[1 << kC9El];
+  pass_load<kC9Log, true, kC9El>(GView<kC9R2, true>{const_cast<u64*>(s), sub}, t, x);
+#ifndef FHE_C9_CHAIN
+#define FHE_C9_CHAIN 0
+#endif
+  pass_run<kC9Log, true, kNotFinal, kBlockSync, false, H, 1, false, FHE_C9_CHAIN != 0, true, false,
+           kC9El>(
+      x, GView<kC9R2>{dst + pm.dst(p) + loc, sub}, lv, t, tw_all + (u64)limb * N, 1u,
+      mods[limb].q, {0, 0}, {0, 0});
+}
+
 // Fused HomMult row kernel: rows of the 4 column-transformed inputs (layout [batch][4][nlimbs][N]
 // in `x`: A0, A1, B0, B1) -> row-forward, tensor, row-inverse -> d [batch][3][nlimbs][N].
 // Thread groups g = 0..3 own one polynomial each; after the forward rows every group writes its
@@ -968,7 +1039,11 @@ struct HmGeo {
 constexpr bool kHmNT = true;
 constexpr bool kKsNT = true;
 
-template <int LOGN, int HR = 8>
+// S9 (N = 2^16, after k_hm_col9): the forward rows are the 512 x 128 split's 7-stage rows, two
+// per 256-word row (its 16 threads: 8 per half), with twf the d_tw_fwd9 layout; the tensor and the
+// inverse are unchanged (the forward's last values go to LDS in its own layout, the tensor reads
+// them in the inverse's first-round layout).
+template <int LOGN, int HR = 8, bool S9 = false>
 __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
                                                           u64* __restrict__ d, u32 nlimbs,
                                                           u32 limb0,
@@ -1008,33 +1083,79 @@ __global__ FHE_KATTR void k_hommult_row(const u64* __restrict__ x,
 
   // forward row pass: round 0 from global, rounds exchange through LDS, last round stays in VGPRs
   u64 v[kE];
-  static_for<0, Rd::NR>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    constexpr int KB = Rd::kb(k);
-    constexpr int LO = Rd::lo_fwd(k);
-    // wide moduli: canonical forward outputs (4 q^2 would exceed q R for q > 2^62)
-    constexpr int F = (k == Rd::NR - 1) ? (HR == 2 ? kFinalFwd : kFinalFwd2) : kNotFinal;
-    constexpr int RIN = fwd_range(fwd_range(1, G::N1, HR), G::N2 - (LO + KB), HR);
-    using Lay = Layout<G::N2, KB, LO>;
-    const u32 tp = Lay::tpos(t);
-    if constexpr (k == 0) {
-      const GView<1, kHmNT> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
-      gin.template load<Lay>(v, tp);
-    } else {
-      lds_sync<SY>();
-      own.template load<Lay>(v, tp);
-    }
-    round_compute<G::N2, KB, LO, true, F, true, HR, RIN>(v, tp, tf, base, q, {0, 0}, {0, 0});
-    if constexpr (k < Rd::NR - 1) {
-      if (k > 0) lds_sync<SY>();
-      own.template store<Lay>(v, tp);
-    }
-  });
-  // tensor: publish canonical A0, A1, B0, B1 at the last forward layout, combine per position
-  using LayT = Layout<G::N2, Rd::kb(Rd::NR - 1), Rd::lo_fwd(Rd::NR - 1)>;
+  // the tensor reads every slot in the inverse's first-round layout (the 256 split's last forward
+  // layout as well)
+  using LayT = Layout<G::N2, Rd::kb_inv(0), Rd::lo_inv(0)>;
   const u32 tpT = LayT::tpos(t);
-  lds_sync<SY>();
-  own.template store<LayT>(v, tpT);
+  if constexpr (S9) {
+    static_assert(LOGN == 16, "the 512 x 128 split is built for N = 2^16");
+    // rounds of 3 + 4 stages: the first round's elements pair into adjacent words (its spare
+    // element bit is position 0), so it loads 16-byte pairs, 256 contiguous bytes per row; the
+    // last round is the 16-element low-bit round of the 256 split (lane-major twiddles, kb 4)
+    using R7 = Rounds<G::N2 - 1, kElog, true>;
+    static_assert(R7::NR == 2 && R7::kb(0) == 3 && R7::lo_fwd(0) == 4 && R7::lo_fwd(1) == 0,
+                  "3 + 4 stages");
+    const u32 h7 = t >> 3, t7 = t & 7;  // half of the 256-word row, thread within it
+    const LView<1, true> own7{rowlds + grp * G::RS + h7 * (128 + 8)};
+    const u32 base7 = 2u * (u32)G::R1 + 2 * row + h7;  // row 2 row + h7 of the 512-row view
+    const ulonglong2* tf9 = twf + (u64)limb * N;
+    static_for<0, R7::NR>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int KB = R7::kb(k);
+      constexpr int LO = R7::lo_fwd(k);
+      constexpr int F = (k == R7::NR - 1) ? (HR == 2 ? kFinalFwd : kFinalFwd2) : kNotFinal;
+      constexpr int RIN = fwd_range(fwd_range(1, G::N1 + 1, HR), G::N2 - 1 - (LO + KB), HR);
+      using Lay = Layout<G::N2 - 1, KB, LO>;
+      const u32 tp = Lay::tpos(t7);
+      if constexpr (k == 0) {
+        static_assert(Lay::jpos(kE / 2) == 1, "the spare element bit is position 0");
+        const gptr_u128 gin = (gptr_u128)(const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc +
+                                          h7 * 128 + tp);
+#pragma unroll
+        for (int j = 0; j < kE / 2; ++j) {
+          const u64x2_t w2 = gld<kHmNT>(gin + Lay::jpos(j) / 2);
+          v[j] = w2.x;
+          v[j + kE / 2] = w2.y;
+        }
+      } else {
+        lds_sync<SY>();
+        own7.template load<Lay>(v, tp);
+      }
+      round_compute<G::N2 - 1, KB, LO, true, F, true, HR, RIN>(v, tp, tf9, base7, q, {0, 0},
+                                                                {0, 0});
+      // every round's values back to the slot (the last one's for the tensor)
+      if (k > 0) lds_sync<SY>();
+      own7.template store<Lay>(v, tp);
+    });
+  } else {
+    static_assert(Rd::lo_fwd(Rd::NR - 1) == Rd::lo_inv(0) && Rd::kb(Rd::NR - 1) == Rd::kb_inv(0),
+                  "tensor layout must match the last forward round");
+    static_for<0, Rd::NR>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int KB = Rd::kb(k);
+      constexpr int LO = Rd::lo_fwd(k);
+      // wide moduli: canonical forward outputs (4 q^2 would exceed q R for q > 2^62)
+      constexpr int F = (k == Rd::NR - 1) ? (HR == 2 ? kFinalFwd : kFinalFwd2) : kNotFinal;
+      constexpr int RIN = fwd_range(fwd_range(1, G::N1, HR), G::N2 - (LO + KB), HR);
+      using Lay = Layout<G::N2, KB, LO>;
+      const u32 tp = Lay::tpos(t);
+      if constexpr (k == 0) {
+        const GView<1, kHmNT> gin{const_cast<u64*>(x) + ((u64)b * 4 + grp) * limbN + loc, 0};
+        gin.template load<Lay>(v, tp);
+      } else {
+        lds_sync<SY>();
+        own.template load<Lay>(v, tp);
+      }
+      round_compute<G::N2, KB, LO, true, F, true, HR, RIN>(v, tp, tf, base, q, {0, 0}, {0, 0});
+      if constexpr (k < Rd::NR - 1) {
+        if (k > 0) lds_sync<SY>();
+        own.template store<Lay>(v, tp);
+      }
+    });
+    // tensor: publish canonical A0, A1, B0, B1 at the last forward layout
+    lds_sync<SY>();
+    own.template store<LayT>(v, tpT);
+  }
   lds_sync<ST>();
   // Montgomery products of the forward outputs (in [0, 2q)): t R^-1 in [0, 2q), which the inverse
   // rows take (inputs below 3q); R is folded back in with N^-1 by the column inverse.  d1's sum of
@@ -1924,14 +2045,30 @@ int hommult_dispatch(const fhe_ctx* c, u64* d, const u64* a, const u64* b, u32 b
   if (int rc = check_grid(item_blocks(ic), G::THR_C, 1, 1, "hommult")) return rc;
   if (int rc = check_grid((u64)batch * nlimbs * H::TILES, H::THR, 1, 1, "hommult")) return rc;
   constexpr bool FL = true;  // a, b are read once: non-temporal
-  k_ntt_col<LOGN, true, HD, FL><<<item_grid(ic),
-                                  G::THR_C, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic,
-                                                    c->d_tw_fwd, c->d_nfold, c->d_mods);
-  prof_mark(s, "hm_col_fwd");
   const dim3 gh((u32)((u64)batch * nlimbs * H::TILES));
-  k_hommult_row<LOGN, HD><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd,
-                                                    c->d_tw_inv, c->d_mods);
-  prof_mark(s, "hm_row_tensor");
+  // N = 2^16: the forward split 9 + 7 (k_hm_col9: 32 elements per thread, the row kernel's
+  // forward rows one stage shorter); other sizes 8 + 8 (log N / 2 each)
+  bool split9 = false;
+  if constexpr (LOGN == 16 && HD != 2) split9 = c->d_tw_fwd9 != nullptr;
+  if (split9) {
+    if constexpr (LOGN == 16 && HD != 2) {
+      const u64 i9 = (u64)batch * 4 * nlimbs * kC9Tiles;
+      k_hm_col9<HD><<<item_grid(i9), kColThreads, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)i9,
+                                                          c->d_tw_fwd, c->d_mods);
+      prof_mark(s, "hm_col_fwd");
+      k_hommult_row<LOGN, HD, true><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd9,
+                                                          c->d_tw_inv, c->d_mods);
+      prof_mark(s, "hm_row_tensor");
+    }
+  } else {
+    k_ntt_col<LOGN, true, HD, FL><<<item_grid(ic),
+                                    G::THR_C, 0, s>>>(a, b, x, nlimbs, limb0, to_x, (u32)ic,
+                                                      c->d_tw_fwd, c->d_nfold, c->d_mods);
+    prof_mark(s, "hm_col_fwd");
+    k_hommult_row<LOGN, HD><<<gh, H::THR, 0, s>>>(x, d, nlimbs, limb0, c->d_tw_fwd,
+                                                      c->d_tw_inv, c->d_mods);
+    prof_mark(s, "hm_row_tensor");
+  }
   const u64 ii = (u64)batch * 3 * nlimbs * G::TILES_C;
   // the Montgomery tensor left a factor R^-1: fold R in with N^-1 (entries 2, 3 of d_nfold)
   k_ntt_col<LOGN, false, inv_h(HD), kHmNT, kHmNT>

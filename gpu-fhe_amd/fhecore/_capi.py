@@ -113,6 +113,10 @@ def load() -> ctypes.CDLL:
                            "(run `make -C gpu-fhe_amd` or __graft_entry__.build())")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            # an A/B variant built from an older commit (FHECORE_LIB, tools/build_variant.sh) may
+            # lack entry points added since; the in-tree library must export every one
+            if os.environ.get("FHECORE_LIB") and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -95,8 +95,14 @@ def hybrid_plan(L: int, log_n: int, ranks: int, groups: int, rank: int, batch: i
     from ._capi import DistHybrid, check, load
 
     h = DistHybrid()
-    check(load().fhe_dist_hybrid_make(ctypes.byref(h), L, log_n, ranks, groups, rank, batch,
-                                      chunks), "fhe_dist_hybrid_make")
+    lib = load()
+    if groups == 1 and not hasattr(lib, "fhe_dist_hybrid_make"):
+        # an older A/B library (FHECORE_LIB): the limb-only plan is the whole job's
+        h.ranks, h.groups, h.g, h.group, h.shard, h.batch0, h.batch = ranks, 1, ranks, 0, rank, 0, batch
+        h.plan = dist_plan(L, log_n, ranks, rank, batch, chunks)
+        return h
+    check(lib.fhe_dist_hybrid_make(ctypes.byref(h), L, log_n, ranks, groups, rank, batch, chunks),
+          "fhe_dist_hybrid_make")
     return h
 
 

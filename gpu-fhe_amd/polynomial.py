@@ -1,7 +1,8 @@
 """Drop-in for the reference's ``' polynomial'`` module (/root/reference/ polynomial.py:1-5).
 
-The reference file name starts with a space; this one does not, so callers import
-``polynomial`` (or keep ``importlib.import_module(' polynomial')`` pointed at the reference).
+The reference file name starts with a space.  Both names work with this directory on sys.path:
+``import polynomial`` (this file) and the reference's own ``importlib.import_module(' polynomial')``
+(`` polynomial.py`` beside it, leading space included, re-exports this module).
 """
 from primitive import *  # noqa: F401,F403
 from arithmetic import vec_add

@@ -219,18 +219,17 @@ def test_keyswitch_valu_fallback_reads_committed_profile(monkeypatch):
 
 
 def test_rocprof_pmc_skips_under_a_profiler(monkeypatch):
-    """Under a profiler (the rocprofiler tool library in LD_PRELOAD, or its ROCPROF* / ROCP_*
-    settings) a nested rocprofv3 would exec its target after its launcher initialised the GPU --
-    refused on the GPU box (round 4, tools/kspmc.sh).  rocprof_pmc must then return the reason
-    without starting any process."""
+    """Under a profiler (the rocprofiler tool library in LD_PRELOAD) a nested rocprofv3 would exec
+    its target after its launcher initialised the GPU -- refused on the GPU box (round 4,
+    tools/kspmc.sh).  rocprof_pmc must then return the reason without starting any process.
+    ROCPROF* / ROCP_* settings without the preload start nothing and switch nothing off."""
     import subprocess
 
     def no_popen(*a, **k):
         raise AssertionError("rocprof_pmc started a process under a profiler")
 
     monkeypatch.setattr(subprocess, "Popen", no_popen)
-    for var, val in (("LD_PRELOAD", "/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so"),
-                     ("ROCPROF_OUTPUT_PATH", "/tmp/x"), ("ROCP_TOOL_LIBRARIES", "x.so")):
+    for var, val in (("LD_PRELOAD", "/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so"),):
         for k in [k for k in os.environ if k.startswith(("ROCPROF", "ROCP_"))]:
             monkeypatch.delenv(k)
         monkeypatch.delenv("LD_PRELOAD", raising=False)
@@ -244,6 +243,8 @@ def test_rocprof_pmc_skips_under_a_profiler(monkeypatch):
         live, why3 = bench.measure_traffic_live("k_hommult_row", [])
         assert live is None and why3 == why
     assert bench.profiled_parent({"LD_PRELOAD": "/usr/lib/libother.so", "PATH": "/bin"}) is None
+    for stray in ({"ROCPROF_OUTPUT_PATH": "/tmp/x"}, {"ROCP_TOOL_LIBRARIES": "x.so"}):
+        assert bench.profiled_parent(stray) is None
 
 
 def test_keyswitch_traffic_live_sums_kernels(monkeypatch):

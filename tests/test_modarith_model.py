@@ -513,8 +513,8 @@ def test_lazy_gs_round(q):
 _KELOG, _KE = 4, 16
 
 
-def _rounds(logr):
-    nr = (logr + _KELOG - 1) // _KELOG
+def _rounds(logr, el=_KELOG):
+    nr = (logr + el - 1) // el
     kb = [logr // nr + (1 if k < logr % nr else 0) for k in range(nr)]
     lo = []
     hi = logr
@@ -525,18 +525,18 @@ def _rounds(logr):
 
 
 class _Layout:
-    def __init__(self, logr, kb, lo):
-        self.logr, self.kb, self.lo = logr, kb, lo
+    def __init__(self, logr, kb, lo, el=_KELOG):
+        self.logr, self.kb, self.lo, self.el = logr, kb, lo, el
         free = [i for i in range(logr) if not lo <= i < lo + kb]
         self.ex = free
-        self.jmask = self.jpos(_KE - 1)
+        self.jmask = self.jpos((1 << el) - 1)
 
     def jpos(self, j):
         p = 0
         for b in range(self.kb):
             if (j >> b) & 1:
                 p |= 1 << (self.lo + b)
-        for b in range(_KELOG - self.kb):
+        for b in range(self.el - self.kb):
             if (j >> (self.kb + b)) & 1:
                 p |= 1 << self.ex[b]
         return p
@@ -551,8 +551,8 @@ class _Layout:
         return p
 
 
-def _lviewc16(p):
-    return (p >> 1) * 32 + (((p ^ (p >> 4)) & 1) << 4)
+def _lviewc16(p, sw=4):
+    return (p >> 1) * 32 + (((p ^ (p >> sw)) & 1) << 4)
 
 
 def _split_bit(wj, rj):
@@ -627,3 +627,54 @@ def test_half_exchange_layouts(fwd):
                 half = [_lviewc16(_half_pos(lay.tpos(t) | lay.jpos(j), sb)) + sub
                         for sub, t in lanes]
                 assert _bank_cycles(half, write) == _bank_cycles(full, write) == (4 if write else 2)
+
+
+def test_half_exchange_layouts_e32():
+    """k_hm_col9 (the HomMult's 512-row column forward, N = 2^16): 32 elements per thread, rounds of
+    5 + 4 stages, one column = 16 threads; LViewC<16, 5> (swap bit 5).  Every thread ends holding
+    the second round's positions, no phase writes a word twice, every exchange instruction is
+    conflict-free (4 write / 2 read cycles), and a wave's 4 threads of a column share the split bit."""
+    logr, el = 9, 5
+    ke = 1 << el
+    nr, kb, lo = _rounds(logr, el)
+    assert (nr, kb, lo) == (2, [5, 4], [4, 0])
+    W, R = _Layout(logr, kb[0], lo[0], el), _Layout(logr, kb[1], lo[1], el)
+    sb = _split_bit(W.jmask, R.jmask)
+    assert sb == 8
+    S = 1 << sb
+    tps = (1 << logr) // ke
+    assert tps == 16
+    for w in range(4):
+        assert len({bool(R.tpos(t) & S) for t in range(4 * w, 4 * w + 4)}) == 1
+    idx = lambda p: _lviewc16(p, 5)  # noqa: E731
+    x = {t: [W.tpos(t) | W.jpos(j) for j in range(ke)] for t in range(tps)}
+    y = {t: [None] * ke for t in range(tps)}
+    for h in (0, 1):
+        lds, written = {}, set()
+        for t in range(tps):
+            hr = bool(R.tpos(t) & S)
+            for j in range(ke):
+                if bool(W.jpos(j) & S) == (h == 1):
+                    i = idx(_half_pos(W.tpos(t) | W.jpos(j), sb))
+                    assert i not in written and 0 <= i < 4096
+                    written.add(i)
+                    lds[i] = y[t][j] if (h == 1 and not hr) else x[t][j]
+        assert len(written) == 256  # one column's half of the 32 KB buffer
+        for t in range(tps):
+            if bool(R.tpos(t) & S) == (h == 1):
+                for j in range(ke):
+                    if h == 0:
+                        y[t][j] = x[t][j]
+                    x[t][j] = lds[idx(_half_pos(R.tpos(t) | R.jpos(j), sb))]
+    for t in range(tps):
+        assert x[t] == [R.tpos(t) | R.jpos(j) for j in range(ke)]
+    for w in range(4):
+        for j in range(ke):
+            for lay, write in ((W, True), (R, False)):
+                lanes = [(lane % 16, 4 * w + lane // 16) for lane in range(64)]
+                half = [idx(_half_pos(lay.tpos(t) | lay.jpos(j), sb)) + sub for sub, t in lanes]
+                assert _bank_cycles(half, write) == (4 if write else 2), (w, j, write)
+    # the old swap bit (4) would conflict in the second round's reads
+    lanes = [(lane % 16, lane // 16) for lane in range(64)]
+    bad = [_lviewc16(_half_pos(R.tpos(t) | R.jpos(0), sb)) + sub for sub, t in lanes]
+    assert _bank_cycles(bad, False) > 2

@@ -11,6 +11,9 @@
 #   ab:<tag>=<reps>|<bench args>|<variant> ...   same-box A/B (tools/ab_bench.sh) -> <out>/ab_<tag>.txt
 #   bundle=A|B|R                 tools/round_bundle.sh part                -> <out>/
 #   prof:<tag>[=<bench args>]    tools/profile_round.sh of a bench command -> <out>/<tag>/
+#   py:<tag>=<script and args>   any python3 tool (e.g. tools/shard_shape.py --hybrid) -> <out>/<tag>.out
+#   gloo:<tag>=<ranks>|<bench args>  bench.py with <ranks> gloo ranks on this one GPU (the rehearsal
+#                                of the driver's multi-GPU launch)            -> <out>/gloo_<tag>.json
 # example: tools/gpu_session.sh gpurun_out/s1 smoke tests "line:w5=--warmup 5 --steps 20"
 set -o pipefail
 out=${1:?out dir}; shift
@@ -42,6 +45,16 @@ for step in "$@"; do
       cat "$out/ab_$tag.txt" ;;
     bundle)
       bash tools/round_bundle.sh "$out" "$arg" || exit $? ;;
+    py:*)
+      tag=${name#py:}
+      timeout -k 10 600 python3 $arg > "$out/$tag.out" 2> "$out/$tag.err" || { tail -n20 "$out/$tag.err"; exit 1; }
+      tail -n5 "$out/$tag.out" ;;
+    gloo:*)
+      tag=${name#gloo:}; IFS='|' read -r nr bargs <<< "$arg"
+      FHE_BENCH_BACKEND=gloo timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node "$nr" --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus "$nr" \
+        $bargs > "$out/gloo_$tag.json" 2> "$out/gloo_$tag.err" || { tail -n20 "$out/gloo_$tag.err"; exit 1; }
+      cut -c1-400 "$out/gloo_$tag.json" ;;
     prof:*)
       bash tools/profile_round.sh "$out/${name#prof:}" $arg || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
