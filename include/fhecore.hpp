@@ -211,6 +211,17 @@ class Comm {
   fhe_comm_t c_ = nullptr;
 };
 
+// The hybrid partition of a key-switch batch (fhe_dist_hybrid_make): `groups` ciphertext groups of
+// ranks / groups limb shards.  Rank `rank` builds its group's Comm with
+// Comm(group_id, plan.g, plan.shard, device) and key-switches plan.batch ciphertexts from plan.batch0.
+inline fhe_dist_hybrid hybrid_plan(uint32_t L, uint32_t log_n, uint32_t ranks, uint32_t groups,
+                                   uint32_t rank, uint32_t batch, uint32_t chunks = 0) {
+  fhe_dist_hybrid h{};
+  check(fhe_dist_hybrid_make(&h, L, log_n, ranks, groups, rank, batch, chunks),
+        "fhe_dist_hybrid_make");
+  return h;
+}
+
 // Homomorphic operations on one stream.
 class Evaluator {
  public:

@@ -201,6 +201,13 @@ int main() {
         std::printf("FAIL comm shard\n");
         return 1;
       }
+      // hybrid partition helper: 8 ranks as 4 ciphertext groups x 2 limb shards of 33 ciphertexts
+      const fhe_dist_hybrid h = fhe::hybrid_plan(4, 12, 8, 4, 5, 33);
+      if (h.g != 2 || h.group != 2 || h.shard != 1 || h.batch0 != 18 || h.batch != 9 ||
+          h.plan.limb0 != 2 || h.plan.nlimbs != 2) {
+        std::printf("FAIL hybrid plan\n");
+        return 1;
+      }
     }
     std::printf("cpp api ok\n");
     return 0;
