@@ -967,6 +967,8 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src, u64* __restrict
 constexpr int kC9Log = 9, kC9El = 5, kC9R2 = 128, kC9Subs = 16, kC9Tiles = kC9R2 / kC9Subs;
 // occupancy target: 4 waves per SIMD (104 VGPRs, no spill); 5 (96 VGPRs + 60 B of scratch)
 // measured col9 0.389 -> 0.452 ms (profiles/r06_split9_ab.txt)
+// (an exchange by column halves -- waves 0-1 / 2-3 taking turns through a full-column buffer, no
+// pending elements -- still spilled at 5 waves: 0.947 ms, profiles/r06_col9_xhalf_ab.txt)
 #ifndef FHE_C9_WAVES
 #define FHE_C9_WAVES 4
 #endif
@@ -990,18 +992,14 @@ k_hm_col9(const u64* __restrict__ src, const u64* __restrict__ src2, u64* __rest
     pl = it / kC9Tiles;
   }
   const u32 p = pl / nlimbs, l = pl % nlimbs;
-  const u32 sub = threadIdx.x % kC9Subs, t = threadIdx.x / kC9Subs;
-  const LViewC<kC9Subs, 5> lv{lds + sub};
   const u64 loc = (u64)l * N + (u64)tile * kC9Subs;
   const u64* s = (pm.second(p) ? src2 + pm.src2(p) : src + pm.src(p)) + loc;
   const u32 limb = __builtin_amdgcn_readfirstlane(limb0 + l);
   u64 x[1 << kC9El];
+  const u32 sub = threadIdx.x % kC9Subs, t = threadIdx.x / kC9Subs;
+  const LViewC<kC9Subs, 5> lv{lds + sub};
   pass_load<kC9Log, true, kC9El>(GView<kC9R2, true>{const_cast<u64*>(s), sub}, t, x);
-#ifndef FHE_C9_CHAIN
-#define FHE_C9_CHAIN 0
-#endif
-  pass_run<kC9Log, true, kNotFinal, kBlockSync, false, H, 1, false, FHE_C9_CHAIN != 0, true, false,
-           kC9El>(
+  pass_run<kC9Log, true, kNotFinal, kBlockSync, false, H, 1, false, false, true, false, kC9El>(
       x, GView<kC9R2>{dst + pm.dst(p) + loc, sub}, lv, t, tw_all + (u64)limb * N, 1u,
       mods[limb].q, {0, 0}, {0, 0});
 }

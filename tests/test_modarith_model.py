@@ -678,3 +678,4 @@ def test_half_exchange_layouts_e32():
     lanes = [(lane % 16, lane // 16) for lane in range(64)]
     bad = [_lviewc16(_half_pos(R.tpos(t) | R.jpos(0), sb)) + sub for sub, t in lanes]
     assert _bank_cycles(bad, False) > 2
+
