@@ -323,6 +323,19 @@ def test_hommult_limb_window(fc):
     assert (d == coracle.hommult(a, b, ctx.moduli[1:3])).all()
 
 
+@pytest.mark.parametrize("L,limb0,nl,B", [(8, 3, 3, 2), (16, 0, 16, 1), (8, 7, 1, 3), (12, 2, 9, 1)])
+def test_hommult_split9_limb_windows(fc, L, limb0, nl, B):
+    """N = 2^16 takes the 9 + 7 forward split (k_hm_col9 + the 7-stage rows with d_tw_fwd9): limb
+    windows off 0 (the second twiddle table's per-limb offset), limb counts below, above and not a
+    multiple of the 8 XCDs (the row kernel's limb placement), against the C oracle."""
+    ctx = ctx_for(fc, 16, L)
+    mods = ctx.moduli[limb0:limb0 + nl]
+    a = rand(mods, 16, (B, 2), seed=50 + nl)
+    b = rand(mods, 16, (B, 2), seed=60 + nl)
+    d = fc.to_host(ctx.hommult(fc.to_device(a), fc.to_device(b), limb0=limb0))
+    assert (d == coracle.hommult(a, b, mods)).all()
+
+
 # ------------------------------------------------------------------ base conversion / key-switch
 
 def test_baseconv_matches_oracle(fc):
