@@ -92,7 +92,6 @@ struct Rounds {
 // positions; the thread index fills every other bit, ascending.
 template <int LOGR, int KB, int LO, int EL = kElog>
 struct Layout {
-  static constexpr int EB = EL;  // log2 of the elements per thread
   static constexpr int E = 1 << EL;
   static constexpr int ex_pos(int k) {
     int found = 0;
@@ -965,15 +964,12 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src, u64* __restrict
 // HBM-bound pass (the 2^9 x 2^7 split).  Same item placement and poly map as
 // k_ntt_col (a's and b's polys into the 4-slot workspace).
 constexpr int kC9Log = 9, kC9El = 5, kC9R2 = 128, kC9Subs = 16, kC9Tiles = kC9R2 / kC9Subs;
-// occupancy target: 4 waves per SIMD (104 VGPRs, no spill); 5 (96 VGPRs + 60 B of scratch)
-// measured col9 0.389 -> 0.452 ms (profiles/r06_split9_ab.txt)
-// (an exchange by column halves -- waves 0-1 / 2-3 taking turns through a full-column buffer, no
-// pending elements -- still spilled at 5 waves: 0.947 ms, profiles/r06_col9_xhalf_ab.txt)
-#ifndef FHE_C9_WAVES
-#define FHE_C9_WAVES 4
-#endif
+// Occupancy: 4 waves per SIMD (104 VGPRs, no spill).  At 5 (96 VGPRs + 60 B of scratch) the pass
+// took 0.452 instead of 0.389 ms (profiles/r06_split9_ab.txt); an exchange by column halves (waves
+// 0-1 / 2-3 taking turns through a full-column buffer, no pending elements) still spilled at 5
+// waves: 0.947 ms (profiles/r06_col9_xhalf_ab.txt).
 template <int H>
-__global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(FHE_C9_WAVES, 8))) void
+__global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 k_hm_col9(const u64* __restrict__ src, const u64* __restrict__ src2, u64* __restrict__ dst,
           u32 nlimbs, u32 limb0, PolyMap pm, u32 items, const ulonglong2* __restrict__ tw_all,
           const ModParams* __restrict__ mods) {
