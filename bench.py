@@ -882,6 +882,26 @@ def valu_profile():
     return None, None
 
 
+def ks_design_min_bytes(B, nl, L, K, dnum, n):
+    """HBM bytes one fused key-switch call (lz16 path, B ciphertexts, nl own Q-limbs of L, K
+    special limbs, dnum digits) must move with this kernel sequence: every kernel reads its inputs
+    and writes its outputs once, the keys once per batch.  Per kernel: the INTT of
+    d2 (2 passes), ModUp (the gathered sources in, the extended rows out), the P rows' inner
+    product (their extended rows and keys in, both accumulators' P rows out), the P rows' column
+    inverse, ModDown's conversion (P rows in, conv out), the Q rows' inner product + finish
+    (extended rows of the other digits, conv, d2, keys in; both outputs out)."""
+    row = n * 8
+    rows = nl + K
+    intt = 4 * B * nl * row
+    modup = B * (dnum * rows - nl) * row + B * L * row
+    p_inner = B * dnum * K * row + dnum * 2 * K * row + 2 * B * K * row
+    p_colinv = 2 * 2 * B * K * row
+    moddown = 2 * B * K * row + 2 * B * nl * row
+    q_fin = B * nl * (dnum - 1) * row + 2 * B * nl * row + B * nl * row + dnum * 2 * nl * row + \
+        2 * B * nl * row
+    return intt + modup + p_inner + p_colinv + moddown + q_fin
+
+
 class KeyswitchLeg:
     """BASELINE configs[3] through the native multi-GPU path: N = 2^16, L = 16, K = 4, dnum = 4,
     a global batch of `--ks-batch` ciphertexts (one key), limbs sharded over the ranks, INTT +
@@ -1005,6 +1025,13 @@ class KeyswitchLeg:
         alg = rf["alg_bytes_per_launch"]
         rf["traffic"] = total // self.B
         rf["traffic_over_alg"] = round(total / self.B / alg, 3)
+        # against the bytes this kernel sequence must move (each kernel's inputs and outputs once:
+        # the extended basis, the accumulators' P rows, conv, the keys once per batch) -- how much
+        # of traffic_over_alg is the two-pass design and how much is waste
+        dmin = ks_design_min_bytes(self.B, self.shard.nlimbs, self.L, self.K, self.DNUM,
+                                   1 << self.log_n)
+        rf["traffic_design_min"] = dmin // self.B
+        rf["traffic_over_design_min"] = round(total / dmin, 3)
         rf["traffic_per_call_by_kernel"] = {k: int(v) for k, v in sorted(per.items())}
         rf["traffic_source"] = (
             "measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes "

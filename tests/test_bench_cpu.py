@@ -301,3 +301,13 @@ def test_hommult_valu_live_rates_and_clocks(monkeypatch):
     assert r["frac_per_cycle"] == pytest.approx(400 / 600 * 2.4 / 2.0, abs=1e-3)
     monkeypatch.setattr(bench, "rocprof_pmc", lambda *a, **k: (None, None, "skipped: x"))
     assert bench.measure_hommult_valu_live(16, 8, 64, 1.0) == (None, "skipped: x")
+
+
+def test_keyswitch_design_minimum_bytes():
+    """bench.ks_design_min_bytes: the bytes the fused key-switch's kernel sequence must move
+    (DESIGN.md §3).  At the bench shape (B 32, L 16, K 4, dnum 4, N 2^16) 5.989 GB per call, which
+    profiles/r06_bench_keyswitch.json's measured 6.046 GB matches to 1 %; a limb shard moves less."""
+    b = bench.ks_design_min_bytes(32, 16, 16, 4, 4, 1 << 16)
+    assert b == 5989466112
+    assert 6046000000 / b < 1.01
+    assert bench.ks_design_min_bytes(32, 2, 16, 4, 4, 1 << 16) < b / 3
