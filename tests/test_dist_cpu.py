@@ -216,3 +216,16 @@ def test_hybrid_partition_gloo(world, groups):
             assert (k1[i] == refs[b0 + i][1][lo:hi]).all(), (rank, i)
             covered[b0 + i, lo:hi] += 1
     assert (covered == 1).all()
+
+
+def test_hybrid_groups_must_divide_world():
+    """fhecore.dist.hybrid_groups refuses a group count that does not divide the ranks (before any
+    collective), and needs no process group for one rank or one-rank groups."""
+    from fhecore.dist import hybrid_groups
+
+    with pytest.raises(ValueError):
+        hybrid_groups(8, 3)
+    with pytest.raises(ValueError):
+        hybrid_groups(4, 0)
+    assert hybrid_groups(1, 1) is None
+    assert hybrid_groups(4, 4) is None  # g = 1: every group is one rank
