@@ -967,7 +967,8 @@ constexpr int kC9Log = 9, kC9El = 5, kC9R2 = 128, kC9Subs = 16, kC9Tiles = kC9R2
 // Occupancy: 4 waves per SIMD (104 VGPRs, no spill).  At 5 (96 VGPRs + 60 B of scratch) the pass
 // took 0.452 instead of 0.389 ms (profiles/r06_split9_ab.txt); an exchange by column halves (waves
 // 0-1 / 2-3 taking turns through a full-column buffer, no pending elements) still spilled at 5
-// waves: 0.947 ms (profiles/r06_col9_xhalf_ab.txt).
+// waves: 0.947 ms (profiles/r06_col9_xhalf_ab.txt); the second round's twiddles from an LDS copy
+// (either exchange, 4 or 5 waves) 0.43-0.46 ms against 0.40 (profiles/r06_col9_lds_twiddles_ab.txt).
 template <int H>
 __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 k_hm_col9(const u64* __restrict__ src, const u64* __restrict__ src2, u64* __restrict__ dst,
