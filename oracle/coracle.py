@@ -47,6 +47,10 @@ def lib():
         L.oracle_keyswitch.argtypes = [_u64p, _u64p, _u64p, _u64p, _u64p, u32, _u64p, u32, _u64p,
                                        u32, u32]
         L.oracle_keyswitch.restype = None
+        _u32p = ctypes.POINTER(ctypes.c_uint32)
+        L.oracle_rotate_sum_hoisted.argtypes = [_u64p, _u64p, _u32p, u32, _u64p, _u64p, _u64p, u32,
+                                                _u64p, u32, _u64p, u32, u32]
+        L.oracle_rotate_sum_hoisted.restype = None
         for f in (L.port_ntt_fwd, L.port_ntt_inv):
             f.argtypes = [_u64p, u64, u32, _u64p, u32]
             f.restype = None
@@ -208,3 +212,19 @@ def keyswitch(d2, evk_b, evk_a, qs, ps, dnum):
     lib().oracle_keyswitch(_p(ks0), _p(ks1), _p(d2), _p(_u64(evk_b)), _p(_u64(evk_a)),
                            n.bit_length() - 1, _p(qs), qs.size, _p(ps), ps.size, dnum)
     return ks0, ks1
+
+
+def rotate_sum_hoisted(ct, galois, keys_b, keys_a, pts, qs, ps, dnum):
+    """sum_r pts[r] * rot_{galois[r]}(ct), one ModUp and one ModDown (double hoisting; restates
+    pyoracle.rotate_sum_hoisted).  ct [2][L][N] NTT form; keys_* [count][dnum][L+K][N] (any
+    values where galois[r] == 1); pts [count][L+K][N].  Returns [2][L][N]."""
+    ct = _u64(ct)
+    _, L, n = ct.shape
+    g = np.ascontiguousarray(np.asarray(galois, dtype=np.uint32))
+    qs = _u64(qs)
+    ps = _u64(ps)
+    out = np.empty((2, L, n), dtype=np.uint64)
+    lib().oracle_rotate_sum_hoisted(_p(out), _p(ct), g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                    g.size, _p(_u64(keys_b)), _p(_u64(keys_a)), _p(_u64(pts)),
+                                    n.bit_length() - 1, _p(qs), qs.size, _p(ps), ps.size, dnum)
+    return out

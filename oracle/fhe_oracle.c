@@ -408,3 +408,120 @@ void oracle_keyswitch(u64* ks0, u64* ks1, const u64* d2, const u64* evk_b, const
   }
   free(mods); free(c); free(acc0); free(acc1); free(ext); free(tmp); free(dstm);
 }
+
+/* ---------------------------------------------------------------- rotation sum, double hoisting
+ * Restates oracle/pyoracle.py rotate_sum_hoisted (gpu-fhe_amd/csrc/galois.hip
+ * launch_rotate_sum_hoisted): out = sum_r pt_r rot_{gal_r}(ct) with one ModUp of c1 and one
+ * ModDown per accumulator.  ct, out: [2][L][N] NTT form over Q; keys_b, keys_a:
+ * [count][dnum][L+K][N] (ignored where gal_r == 1, the unrotated term); pts: [count][L+K][N]
+ * NTT form over Q u P. */
+static u64 oracle_gather_src(u64 j, u64 k, uint32_t log_n) {
+  const u64 n = 1ull << log_n;
+  const u64 e = (2 * (u64)bitrev((uint32_t)j, log_n) + 1) * k % (2 * n);
+  return bitrev((uint32_t)((e - 1) / 2), log_n);
+}
+
+void oracle_rotate_sum_hoisted(u64* out, const u64* ct, const uint32_t* gal, uint32_t count,
+                               const u64* keys_b, const u64* keys_a, const u64* pts,
+                               uint32_t log_n, const u64* qs, uint32_t L, const u64* ps,
+                               uint32_t K, uint32_t dnum) {
+  const u64 n = 1ull << log_n;
+  const uint32_t LK = L + K, alpha = (L + dnum - 1) / dnum;
+  const u64 ln = (u64)L * n, lkn = (u64)LK * n;
+  const u64* c0 = ct;
+  const u64* c1 = ct + ln;
+  u64* mods = malloc(LK * 8);
+  memcpy(mods, qs, L * 8);
+  memcpy(mods + L, ps, K * 8);
+  prepare(log_n, mods, LK);
+  /* ModUp of c1: every digit extended to Q u P, NTT form (own rows: c1 itself) */
+  u64* ext = malloc((u64)dnum * lkn * 8);
+  u64* c = malloc(ln * 8);
+  u64* tmp = malloc(lkn * 8);
+  u64* dstm = malloc(LK * 8);
+  memcpy(c, c1, ln * 8);
+  oracle_ntt_inv(c, 1, log_n, qs, L);
+  uint32_t nd = 0;
+  for (uint32_t j = 0; j < dnum; ++j) {
+    const uint32_t lo = j * alpha, hi = lo + alpha < L ? lo + alpha : L;
+    if (lo >= L) break;
+    ++nd;
+    uint32_t T = 0;
+    for (uint32_t i = 0; i < LK; ++i)
+      if (i < lo || i >= hi) dstm[T++] = mods[i];
+    oracle_baseconv(tmp, c + (u64)lo * n, n, qs + lo, hi - lo, dstm, T);
+    u64* e = ext + (u64)j * lkn;
+    for (uint32_t i = 0, k = 0; i < LK; ++i) {
+      const u64* src = (i >= lo && i < hi) ? c + (u64)i * n : tmp + (u64)(k++) * n;
+      memcpy(e + (u64)i * n, src, n * 8);
+    }
+    oracle_ntt_fwd(e, 1, log_n, mods, LK);
+  }
+  u64* a0 = calloc(lkn, 8);
+  u64* a1 = calloc(lkn, 8);
+  u64* s0 = calloc(ln, 8);
+  u64* idx = malloc(n * 8);
+  u64 pmod[64];
+  for (uint32_t i = 0; i < L; ++i) {
+    u64 pm = 1;
+    for (uint32_t k = 0; k < K; ++k) pm = mulmod(pm, ps[k] % qs[i], qs[i]);
+    pmod[i] = pm;
+  }
+  for (uint32_t r = 0; r < count; ++r) {
+    const u64* pt = pts + (u64)r * lkn;
+    if (gal[r] == 1) {
+#pragma omp parallel for schedule(static)
+      for (int64_t i = 0; i < (int64_t)L; ++i) {
+        const u64 q = qs[i];
+        for (u64 k = 0; k < n; ++k) {
+          const u64 x = (u64)i * n + k;
+          s0[x] = (u64)(((u128)pt[x] * c0[x] + s0[x]) % q);
+          a1[x] = (u64)(((u128)pt[x] * mulmod(pmod[i], c1[x], q) + a1[x]) % q);
+        }
+      }
+      continue;
+    }
+    for (u64 k = 0; k < n; ++k) idx[k] = oracle_gather_src(k, gal[r], log_n);
+    const u64* kb = keys_b + (u64)r * dnum * lkn;
+    const u64* ka = keys_a + (u64)r * dnum * lkn;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)LK; ++i) {
+      const u64 q = mods[i];
+      for (u64 k = 0; k < n; ++k) {
+        const u64 x = (u64)i * n + k, xs = (u64)i * n + idx[k];
+        u64 t0 = 0, t1 = 0;
+        for (uint32_t j = 0; j < nd; ++j) {
+          const u64 v = ext[(u64)j * lkn + xs];
+          t0 = (u64)(((u128)v * kb[(u64)j * lkn + x] + t0) % q);
+          t1 = (u64)(((u128)v * ka[(u64)j * lkn + x] + t1) % q);
+        }
+        a0[x] = (u64)(((u128)pt[x] * t0 + a0[x]) % q);
+        a1[x] = (u64)(((u128)pt[x] * t1 + a1[x]) % q);
+        if (i < (int64_t)L) s0[x] = (u64)(((u128)pt[x] * c0[xs] + s0[x]) % q);
+      }
+    }
+  }
+  /* one ModDown per accumulator; out0 = s0 + ModDown(a0), out1 = ModDown(a1) */
+  u64 pinv[64];
+  for (uint32_t i = 0; i < L; ++i) pinv[i] = powmod(pmod[i], qs[i] - 2, qs[i]);
+  u64* xp = malloc((u64)K * n * 8);
+  for (int which = 0; which < 2; ++which) {
+    const u64* acc = which ? a1 : a0;
+    u64* o = out + (u64)which * ln;
+    memcpy(xp, acc + ln, (u64)K * n * 8);
+    oracle_ntt_inv(xp, 1, log_n, ps, K);
+    oracle_baseconv(tmp, xp, n, ps, K, qs, L);
+    oracle_ntt_fwd(tmp, 1, log_n, qs, L);
+    for (uint32_t i = 0; i < L; ++i) {
+      const u64 q = qs[i];
+      for (u64 k = 0; k < n; ++k) {
+        const u64 x = (u64)i * n + k, y = tmp[x], v = acc[x];
+        u64 m = mulmod(v >= y ? v - y : v + q - y, pinv[i], q);
+        if (!which) m = (u64)(((u128)m + s0[x]) % q);
+        o[x] = m;
+      }
+    }
+  }
+  free(xp); free(idx); free(a0); free(a1); free(s0);
+  free(mods); free(c); free(ext); free(tmp); free(dstm);
+}

@@ -611,6 +611,58 @@ def rotate_hoisted(ct_ntt, ks, keys, qs, ps, dnum, log_n: int):
     return np.stack(out)
 
 
+def rotate_sum_hoisted(ct_ntt, ks, keys, pts, qs, ps, dnum, log_n: int):
+    """sum_r pt_r * rot_{k_r}(ct) with one ModUp and one ModDown (double hoisting, the inner
+    loop of a baby-step / giant-step linear transform), restated for gpu-fhe_amd/csrc/galois.hip
+    launch_rotate_sum_hoisted.  pts[r]: (L + K, N) NTT form over Q u P.  Per rotation the
+    key-switch accumulators of rotate_hoisted are multiplied by pt_r and summed in Q u P;
+    sigma_k(c0) times pt_r is summed over Q; ModDown runs once on each summed accumulator:
+      out = (sum_r pt_r sigma_r(c0) + ModDown(A0), ModDown(A1)),
+      A_h = sum_r pt_r acc_h^(r).
+    k_r = 1 is the unrotated term (no key; keys[r] may be None): pt_r c0 joins the c0 sum and
+    pt_r (P mod q_i) c1 joins A1's Q rows, so that ModDown returns pt_r c1 exactly
+    (ModDown(P x + y) = x + ModDown(y)).  Decrypts to sum_r pt_r sigma_r(m) up to one ModDown's
+    rounding, not to the sum of separate rotate_hoisted outputs bit for bit.  (L, N) x 2 out."""
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    allm = qs + ps
+    L = len(qs)
+    P = math.prod(ps)
+    c0 = np.asarray(ct_ntt[0]).astype(object)
+    c1 = np.asarray(ct_ntt[1]).astype(object)
+    n = c1.shape[-1]
+    mods = _mods_col(allm)
+    col = _mods_col(qs)
+    ext = None
+    if any(int(k) != 1 for k in ks):
+        ext = [rns_ntt_fwd(e, allm) for e in modup(rns_ntt_inv(c1, qs), qs, ps, dnum)]
+        for (lo, hi), e in zip(digit_ranges(L, dnum), ext):
+            e[lo:hi] = c1[lo:hi]
+    a0 = np.zeros((len(allm), n), dtype=object)
+    a1 = np.zeros_like(a0)
+    s0 = np.zeros((L, n), dtype=object)
+    pcol = np.array([P % q for q in qs], dtype=object).reshape(-1, 1)
+    for k, key, pt in zip(ks, keys, pts):
+        k = int(k)
+        pt = np.asarray(pt).astype(object)
+        if k == 1:
+            s0 = (s0 + pt[:L] * c0) % col
+            a1[:L] = (a1[:L] + pt[:L] * (pcol * c1 % col)) % col
+            continue
+        rot_b, rot_a = key
+        idx = automorphism_ntt_index(k, log_n)
+        acc0 = np.zeros((len(allm), n), dtype=object)
+        acc1 = np.zeros_like(acc0)
+        for j, e in enumerate(ext):
+            g = e[..., idx]
+            acc0 = (acc0 + g * np.asarray(rot_b[j]).astype(object)) % mods
+            acc1 = (acc1 + g * np.asarray(rot_a[j]).astype(object)) % mods
+        a0 = (a0 + pt * acc0) % mods
+        a1 = (a1 + pt * acc1) % mods
+        s0 = (s0 + pt[:L] * c0[..., idx]) % col
+    return np.stack([(s0 + moddown_ntt(a0, qs, ps)) % col, moddown_ntt(a1, qs, ps)])
+
+
 def rescale_coeff(x, moduli):
     """Divide-and-round by the last modulus: x (l, N) coefficient form over q_0..q_{l-1} ->
     (l - 1, N) with out_i = floor((X + q_last // 2) / q_last) mod q_i, X the CRT value in

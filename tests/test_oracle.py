@@ -285,6 +285,63 @@ def test_hoisted_rotations_decrypt_to_rotated_messages(dnum):
         assert max(abs(int(x) - int(y)) for x, y in zip(dec, dref)) < 1 << 20
 
 
+def _negacyclic_int(a, b):
+    """a b in Z[X]/(X^N + 1), plain integers."""
+    n = len(a)
+    out = [0] * n
+    for i, x in enumerate(a):
+        if x:
+            for j, y in enumerate(b):
+                k = i + j
+                if k < n:
+                    out[k] += x * y
+                else:
+                    out[k - n] -= x * y
+    return out
+
+
+@pytest.mark.parametrize("dnum", [3, 2])
+def test_rotation_sum_double_hoisted_decrypts(dnum):
+    """pyoracle.rotate_sum_hoisted (one ModUp, one ModDown for sum_r pt_r rot_r(ct), the inner
+    loop of a BSGS linear transform) decrypts to sum_r pt_r sigma_r(m) + small noise, including the
+    unrotated term (Galois element 1, no key), and the C restatement matches it word for word."""
+    log_n, L, K = 5, 3, 2
+    n = 1 << log_n
+    mods = pyoracle.gen_moduli(log_n, L + K)
+    qs, ps = mods[:L], mods[L:]
+    allm = qs + ps
+    rng = random.Random(51 + dnum)
+    s = [rng.randrange(-1, 2) for _ in range(n)]
+    m = [rng.randrange(-1000, 1000) for _ in range(n)]
+    col = pyoracle._mods_col(qs)
+    s_n = pyoracle.rns_ntt_fwd(pyoracle._to_rns(s, qs), qs)
+    a = np.stack([np.array([rng.randrange(q) for _ in range(n)], dtype=object) for q in qs])
+    e = pyoracle.rns_ntt_fwd(pyoracle._to_rns([rng.randrange(-3, 4) for _ in range(n)], qs), qs)
+    m_n = pyoracle.rns_ntt_fwd(pyoracle._to_rns(m, qs), qs)
+    ct = np.stack([(-a * s_n + e + m_n) % col, a])
+    ks = [1, pyoracle.galois_elt(1, n), pyoracle.galois_elt(-3, n), 2 * n - 1]
+    keys = [None if k == 1 else pyoracle.gen_rot_key(s, k, qs, ps, dnum, rng) for k in ks]
+    pt_int = [[rng.randrange(-3, 4) for _ in range(n)] for _ in ks]
+    pts = [pyoracle.rns_ntt_fwd(pyoracle._to_rns(p, allm), allm) for p in pt_int]
+    out = pyoracle.rotate_sum_hoisted(ct, ks, keys, pts, qs, ps, dnum, log_n)
+    assert out.shape == (2, L, n)
+    dec = pyoracle.crt_centered(pyoracle.rns_ntt_inv((out[0] + out[1] * s_n) % col, qs), qs)
+    want = [0] * n
+    for k, p in zip(ks, pt_int):
+        mk = pyoracle.automorphism_coeff(np.array([[v % qs[0] for v in m]], dtype=object), k,
+                                         [qs[0]])[0]
+        mk = [int(v) - qs[0] if int(v) > qs[0] // 2 else int(v) for v in mk]
+        want = [w + v for w, v in zip(want, _negacyclic_int(p, mk))]
+    assert max(abs(int(d) - w) for d, w in zip(dec, want)) < 1 << 24
+    # the C restatement, word for word (keys of the unrotated term: any words, ignored)
+    zero = np.zeros((dnum, L + K, n), dtype=np.uint64)
+    kb = np.stack([zero if kk is None else np.asarray(kk[0], dtype=np.uint64) for kk in keys])
+    ka = np.stack([zero if kk is None else np.asarray(kk[1], dtype=np.uint64) for kk in keys])
+    got = coracle.rotate_sum_hoisted(np.asarray(ct, dtype=np.uint64), ks, kb, ka,
+                                     np.asarray(pts, dtype=np.uint64), qs, ps, dnum)
+    assert (got.astype(object) == out).all()
+
+
 # ---- SURVEY.md §8(f) row 3: Philox and samplers ---------------------------------------------
 
 def test_philox_known_answers():
