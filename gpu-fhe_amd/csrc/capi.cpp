@@ -402,6 +402,43 @@ int fhe_rotate_hoisted(const fhe_ctx* c, uint64_t* out, const uint64_t* in,
   return launch_rotate_hoisted(c, out, in, galois_elts, rot_b, rot_a, count, batch, ws, hs(s));
 }
 
+size_t fhe_rotate_sum_hoisted_workspace(const fhe_ctx* c, uint32_t batch) {
+  return c ? rotate_sum_hoisted_workspace_bytes(c, batch) : 0;
+}
+
+int fhe_rotate_sum_hoisted(const fhe_ctx* c, uint64_t* out, const uint64_t* in,
+                           const uint32_t* galois_elts, const uint64_t* const* rot_b,
+                           const uint64_t* const* rot_a, const uint64_t* const* pt,
+                           uint32_t count, uint32_t batch, void* ws, fhe_stream_t s) {
+  int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_rotate_sum_hoisted");
+  if (rc) return rc;
+  if (count == 0 || count > kRotSumMax) {
+    set_error("fhe_rotate_sum_hoisted: count must be 1..16");
+    return kInvalid;
+  }
+  if (!galois_elts || !pt || ((!rot_b || !rot_a) && std::any_of(galois_elts, galois_elts + count,
+                                                                 [](uint32_t g) { return g != 1; }))) {
+    set_error("fhe_rotate_sum_hoisted: null Galois element, plaintext or key array");
+    return kInvalid;
+  }
+  for (uint32_t r = 0; r < count; ++r) {
+    // the kernels would dereference them on the device; the unrotated term (1) takes no key
+    if (!pt[r] || (galois_elts[r] != 1 && (!rot_b[r] || !rot_a[r]))) {
+      set_error("fhe_rotate_sum_hoisted: null plaintext or key pointer for term " +
+                std::to_string(r));
+      return kInvalid;
+    }
+  }
+  const uint64_t span = (uint64_t)batch * 2 * c->L * c->n;
+  if (spans_overlap(out, span, in, span)) {
+    set_error("fhe_rotate_sum_hoisted: out must not overlap in");
+    return kInvalid;
+  }
+  if ((rc = ensure_ws(c, rotate_sum_hoisted_workspace_bytes(c, batch), &ws, hs(s)))) return rc;
+  return launch_rotate_sum_hoisted(c, out, in, galois_elts, rot_b, rot_a, pt, count, batch, ws,
+                                   hs(s));
+}
+
 size_t fhe_mul_relin_workspace(const fhe_ctx* c, uint32_t batch) {
   return c ? mul_relin_workspace_bytes(c, batch) : 0;
 }

@@ -112,6 +112,119 @@ inline u32 modinv_odd_pow2(u32 k, u32 bits) {
   return inv & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1));
 }
 
+
+// Double-hoisted rotation sum (launch_rotate_sum_hoisted): the per-rotation inner products of the
+// hoisted rotations, each times its plaintext pt_r and summed in Q u P, so that one ModDown serves
+// every term:  A_h = sum_r pt_r sum_j sigma_r(ext_j) evk_r,h[j],  C0 = sum_r pt_r sigma_r(c0),
+// and for the unrotated term (gal 1, no key) C0 += pt c0, C1 += pt c1 (ModDown(P pt c1 + y) =
+// pt c1 + ModDown(y) exactly, so pt c1 joins out_1 after ModDown instead).  Restated by
+// oracle/pyoracle.py rotate_sum_hoisted.
+// One thread = one position (row r of Q u P, coefficient i) for kRotSumBC ciphertexts, so each
+// key word is loaded once for them; the kRotSumBC-ciphertext groups of one (row, 256 positions)
+// are dealt to one XCD back to back (their key words then come from its L2).  The NTT-domain
+// gather maps every aligned 64-slot block onto one aligned 64-slot block (brv(src) =
+// brv(i) k + (k - 1) / 2 mod N: the top bits of brv(i) only reach the top bits of the product),
+// so each wavefront's gathered loads stay within 512 contiguous bytes.
+struct RotSumTerms {
+  u32 count;
+  u32 gal[kRotSumMax];
+  const u64* kb[kRotSumMax];
+  const u64* ka[kRotSumMax];
+  const u64* pt[kRotSumMax];
+};
+constexpr u32 kRotSumBC = 4;
+
+// a + x y for the rotation sum's 128-bit accumulators: narrow moduli (q < 2^61) add exact
+// products (at most 16 terms of q^2 < 2^122 each); wide ones reduce every product
+template <bool WIDE>
+__device__ __forceinline__ void rs_mac(u128& a, u64 x, u64 y, const ModParams& m) {
+  const u128 p = (u128)x * y;
+  if constexpr (WIDE) {
+    a = csub((u64)a + reduce128_wide((u64)p, (u64)(p >> 64), m), m.q);
+  } else {
+    a += p;
+  }
+}
+template <bool WIDE>
+__device__ __forceinline__ u64 rs_fin(u128 a, const ModParams& m) {
+  if constexpr (WIDE) return (u64)a;
+  return reduce128((u64)a, (u64)(a >> 64), m);
+}
+
+template <int DNUM, bool WIDE>
+__global__ __launch_bounds__(kThreads) void k_rot_sum(u64* __restrict__ acc, u64 acc_ws,
+                                                      u64* __restrict__ cadd, int ident,
+                                                      const u64* __restrict__ ext,
+                                                      const u64* __restrict__ in,
+                                                      const RotSumTerms tm, u32 rows, u32 L,
+                                                      u32 alpha, u32 batch, u32 log_n,
+                                                      const ModParams* __restrict__ mods) {
+  const u64 n = 1ull << log_n, rn = (u64)rows * n, ln = (u64)L * n;
+  const u32 per_row = (u32)(n / kThreads), nbc = (batch + kRotSumBC - 1) / kRotSumBC;
+  const u32 xcd = blockIdx.x % 8, k8 = blockIdx.x / 8;
+  const u32 bc = k8 % nbc, item = (k8 / nbc) * 8 + xcd;
+  if (item >= rows * per_row) return;  // grid rounded up to whole groups of 8
+  const u32 r = item / per_row;
+  const u64 i = (u64)(item % per_row) * kThreads + threadIdx.x;
+  const u64 e = (u64)r * n + i;
+  const ModParams m = mods[r];  // rows = the context's L + K limbs in order
+  const u32 own = r < L ? r / alpha : 0xffffffffu;
+  const u32 b0 = bc * kRotSumBC, nb = min(kRotSumBC, batch - b0);
+  u128 s0[kRotSumBC] = {}, s1[kRotSumBC] = {}, a0[kRotSumBC] = {}, a1[kRotSumBC] = {};
+  const u32 sh = 32 - log_n, mask2 = (2u << log_n) - 1;
+  for (u32 k = 0; k < tm.count; ++k) {
+    const u32 g = tm.gal[k];
+    const u64 p = tm.pt[k][e];
+    if (g == 1) {  // the unrotated term (workgroup-uniform)
+      if (r < L) {
+#pragma unroll
+        for (u32 bb = 0; bb < kRotSumBC; ++bb) {
+          if (bb >= nb) break;
+          const u64* ct = in + (u64)(b0 + bb) * 2 * ln + e;
+          rs_mac<WIDE>(a0[bb], p, ct[0], m);
+          rs_mac<WIDE>(a1[bb], p, ct[ln], m);
+        }
+      }
+      continue;
+    }
+    const u32 gi = ((2 * (__builtin_bitreverse32((u32)i) >> sh) + 1) * g) & mask2;
+    const u64 si = __builtin_bitreverse32((gi - 1) >> 1) >> sh;
+    const u64 es = (u64)r * n + si;
+    u64 kb[DNUM], ka[DNUM];
+#pragma unroll
+    for (int j = 0; j < DNUM; ++j) {
+      kb[j] = tm.kb[k][(u64)j * rn + e];
+      ka[j] = tm.ka[k][(u64)j * rn + e];
+    }
+#pragma unroll
+    for (u32 bb = 0; bb < kRotSumBC; ++bb) {
+      if (bb >= nb) break;
+      const u32 b = b0 + bb;
+      u128 t0 = 0, t1 = 0;
+#pragma unroll
+      for (int j = 0; j < DNUM; ++j) {
+        const u64 x = (u32)j == own ? in[(u64)b * 2 * ln + ln + es]
+                                    : ext[((u64)j * batch + b) * rn + es];
+        rs_mac<WIDE>(t0, x, kb[j], m);
+        rs_mac<WIDE>(t1, x, ka[j], m);
+      }
+      rs_mac<WIDE>(s0[bb], p, rs_fin<WIDE>(t0, m), m);
+      rs_mac<WIDE>(s1[bb], p, rs_fin<WIDE>(t1, m), m);
+      if (r < L) rs_mac<WIDE>(a0[bb], p, in[(u64)b * 2 * ln + es], m);
+    }
+  }
+#pragma unroll
+  for (u32 bb = 0; bb < kRotSumBC; ++bb) {
+    if (bb >= nb) break;
+    const u32 b = b0 + bb;
+    acc[(u64)b * rn + e] = rs_fin<WIDE>(s0[bb], m);
+    acc[acc_ws + (u64)b * rn + e] = rs_fin<WIDE>(s1[bb], m);
+    if (r < L) {
+      cadd[(u64)b * ln + e] = rs_fin<WIDE>(a0[bb], m);
+      if (ident) cadd[(u64)(batch + b) * ln + e] = rs_fin<WIDE>(a1[bb], m);
+    }
+  }
+}
 }  // namespace
 
 int build_galois_tables(fhe_ctx* c) {
@@ -324,6 +437,103 @@ int launch_rotate_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* 
       return rc;
   }
   return kOk;
+}
+
+size_t rotate_sum_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch) {
+  // c1's coefficient form [batch][L][N], the c0 / c1 addends [2][batch][L][N], the fused ModDown's
+  // INTT output [2 batch][K][N], then the key-switch workspace (ext digits, accumulators)
+  return (3 * (size_t)c->L + 2 * (size_t)c->K) * batch * c->n * sizeof(u64) +
+         keyswitch_workspace_bytes(c, c->L, batch);
+}
+
+// Double hoisting (the inner loop of a baby-step / giant-step linear transform): ModUp(c1) once
+// (as launch_rotate_hoisted), one k_rot_sum pass that forms every rotation's inner product through
+// its automorphism, multiplies it by pt_r and sums the terms in Q u P, then ONE ModDown per
+// accumulator with the c0 (and unrotated c1) sums added in its finish.  Against count hoisted
+// rotations + count plaintext products + a sum, it saves count - 1 ModDowns and every per-rotation
+// output round trip.  Restated by oracle/pyoracle.py rotate_sum_hoisted.
+int launch_rotate_sum_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* galois,
+                              const u64* const* rot_b, const u64* const* rot_a,
+                              const u64* const* pt, u32 count, u32 batch, void* ws,
+                              hipStream_t s) {
+  if (c->K == 0) {
+    set_error("rotate_sum_hoisted: context has no special primes (K = 0)");
+    return kInvalid;
+  }
+  if (count > kRotSumMax) {
+    set_error("rotate_sum_hoisted: at most 16 terms per call");
+    return kInvalid;
+  }
+  if (c->dnum > 8) {
+    set_error("rotate_sum_hoisted: dnum > 8");
+    return kUnsupported;
+  }
+  const u32 two_n = 2u << c->log_n;
+  RotSumTerms tm{};
+  tm.count = count;
+  bool ident = false, rotated = false;
+  for (u32 r = 0; r < count; ++r) {
+    if ((galois[r] & 1) == 0 || galois[r] >= two_n) {
+      set_error("rotate_sum_hoisted: every Galois element must be odd and below 2N");
+      return kInvalid;
+    }
+    tm.gal[r] = galois[r];
+    tm.kb[r] = rot_b[r];
+    tm.ka[r] = rot_a[r];
+    tm.pt[r] = pt[r];
+    ident = ident || galois[r] == 1;
+    rotated = rotated || galois[r] != 1;
+  }
+  if (batch == 0) return kOk;
+  const u32 L = c->L, K = c->K, rows = L + K;
+  const u64 n = c->n, ln = (u64)L * n;
+  u64* c_all = static_cast<u64*>(ws);  // [batch][L][N] coefficient form of c1
+  u64* cadd = c_all + batch * ln;      // [2][batch][L][N]
+  u64* ydn = cadd + 2 * batch * ln;    // [2 batch][K][N]
+  u64* kws = ydn + 2 * batch * (u64)K * n;
+  const u64 blocks = (u64)rows * (n / kThreads);
+  const u64 grid = (blocks + 7) / 8 * 8 * ((batch + kRotSumBC - 1) / kRotSumBC);
+  if (int rc = check_grid(grid, kThreads, 1, 1, "rotate_sum_hoisted")) return rc;
+  int rc;
+  const CAll call = CAll::contiguous(c_all, L, n);
+  if (rotated) {
+    if ((rc = launch_ntt_strided(c, false, in + ln, 2 * ln, c_all, ln, batch, 0, L, s))) return rc;
+    KsHoist up;
+    up.modup_only = true;
+    if ((rc = launch_keyswitch_shard(c, nullptr, nullptr, call, in + ln, nullptr, nullptr, 0, L,
+                                     batch, kws, s, nullptr, &up)))
+      return rc;
+  }
+  u64* acc = ks_acc_region(c, kws, L, batch);
+  const u64 acc_ws = (u64)batch * rows * n;
+  const u64* ext = static_cast<const u64*>(kws);
+  switch (c->dnum) {
+#define X(d)                                                                                      \
+  case d:                                                                                         \
+    if (c->wide)                                                                                  \
+      k_rot_sum<d, true><<<dim3((u32)grid), kThreads, 0, s>>>(acc, acc_ws, cadd, ident, ext, in, \
+                                                               tm, rows, L, c->alpha, batch,      \
+                                                               c->log_n, c->d_mods);              \
+    else                                                                                          \
+      k_rot_sum<d, false><<<dim3((u32)grid), kThreads, 0, s>>>(                                   \
+          acc, acc_ws, cadd, ident, ext, in, tm, rows, L, c->alpha, batch, c->log_n, c->d_mods);  \
+    break;
+    X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+#undef X
+  }
+  FHE_HIP_CHECK(hipGetLastError());
+  prof_mark(s, "rot_sum");
+  // ModDown of both sums; out_0 += C0, out_1 += C1 (the unrotated term's pt c1) in its finish
+  KsHoist h;
+  h.acc_ready = true;
+  h.ydn = ydn;
+  KsEpilogue ep;
+  ep.out_bs = 2 * ln;
+  ep.add0 = cadd;
+  ep.add1 = ident ? cadd + batch * ln : nullptr;
+  ep.add_bs = ln;
+  return launch_keyswitch_shard(c, out, out + ln, call, in + ln, nullptr, nullptr, 0, L, batch, kws,
+                                s, &ep, &h);
 }
 
 }  // namespace fhe

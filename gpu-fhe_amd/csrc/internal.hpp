@@ -228,7 +228,15 @@ struct KsHoist {
   bool modup_only = false;
   u32 galois = 0;
   u64* ydn = nullptr;  // [2 batch][K][N] scratch for the fused ModDown (the ext region is taken)
+  // the caller has filled the accumulators (ks_acc_region) itself: ModDown only (the rotation
+  // sum, galois.hip launch_rotate_sum_hoisted)
+  bool acc_ready = false;
 };
+// The key-switch workspace's regions (keyswitch_workspace_bytes): ext [dnum][batch][rows][N], then
+// the accumulators acc [2][batch][rows][N], rows = nlimbs + K
+inline u64* ks_acc_region(const fhe_ctx* c, void* ws, u32 nlimbs, u32 batch) {
+  return static_cast<u64*>(ws) + (u64)c->dnum * batch * (nlimbs + c->K) * c->n;
+}
 struct ModDownRowArgs {
   const u64* conv;
   u64* ks0;
@@ -367,6 +375,15 @@ int launch_rotate_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* 
                           const u64* const* rot_b, const u64* const* rot_a, u32 count, u32 batch,
                           void* ws, hipStream_t s);
 size_t rotate_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch);
+// Double-hoisted rotation sum: out [batch][2][L][N] = sum_r pt[r] rot_{galois[r]}(in), one ModUp
+// and one ModDown; pt[r] [L + K][N] NTT form (host array of device pointers); galois[r] == 1 is
+// the unrotated term (no key).  count <= kRotSumMax.
+constexpr u32 kRotSumMax = 16;
+int launch_rotate_sum_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* galois,
+                              const u64* const* rot_b, const u64* const* rot_a,
+                              const u64* const* pt, u32 count, u32 batch, void* ws,
+                              hipStream_t s);
+size_t rotate_sum_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch);
 
 // ---- launchers (pipeline.hip): SURVEY.md §8(f) row 4 -----------------------------------
 int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, const u64* evk_b,

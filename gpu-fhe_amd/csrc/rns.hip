@@ -570,7 +570,7 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     if ((rc = launch_ks_row_inner(c, ka, s))) return rc;
   }
   const dim3 gi((u32)(n / kThreads), rows);
-  if (!fused) switch (c->dnum) {
+  if (!fused && !(hoist && hoist->acc_ready)) switch (c->dnum) {
 #define X(k)                                                                                     \
   case k:                                                                                        \
     k_ks_inner<k><<<gi, kThreads, 0, s>>>(acc, acc_ws, ext, d2_own, evk_b, evk_a, rows, nlimbs, \

@@ -386,6 +386,50 @@ class Context:
                   "fhe_rotate_hoisted")
         return out
 
+    def rotate_sum_hoisted(self, ct, galois_elts, rot_keys, pts, workspace=None, out=None):
+        """sum_r pts[r] * rot_{galois_elts[r]}(ct) for ct [..., 2, L, N] (NTT form) with one ModUp
+        and one ModDown (fhe_rotate_sum_hoisted, double hoisting): rot_keys[r] = (rot_b, rot_a)
+        [dnum, L + K, N], or None for the unrotated term (Galois element 1); pts[r] [L + K, N]
+        NTT form over Q u P.  Returns [..., 2, L, N]."""
+        _check_tensor(ct, "ct", (2, self.L, self.n))
+        elts = [int(g) for g in galois_elts]
+        count = len(elts)
+        if len(rot_keys) != count or len(pts) != count:
+            raise ValueError("rotate_sum_hoisted: one key (or None) and one plaintext per term")
+        for g, key, pt in zip(elts, rot_keys, pts):
+            if tuple(pt.shape) != (self.L + self.K, self.n) or pt.device != ct.device or not \
+                    pt.is_contiguous():
+                raise ValueError("rotate_sum_hoisted: plaintexts must be contiguous [L + K, N] "
+                                 "on the ct's device")
+            if key is None:
+                if g != 1:
+                    raise ValueError("rotate_sum_hoisted: only Galois element 1 takes no key")
+                continue
+            kb, ka = key
+            if tuple(kb.shape) != (self.dnum, self.L + self.K, self.n) or ka.shape != kb.shape:
+                raise ValueError("rotate_sum_hoisted: keys must be [dnum, L + K, N]")
+            if kb.device != ct.device or ka.device != ct.device or not (
+                    kb.is_contiguous() and ka.is_contiguous()):
+                raise ValueError("rotate_sum_hoisted: keys must be contiguous on the ct's device")
+        batch = ct.numel() // (2 * self.L * self.n)
+        if out is None:
+            out = _empty(*ct.shape, dtype=ct.dtype, device=ct.device)
+        else:
+            _check_out(out, ct, tuple(ct.shape), "rotate_sum_hoisted: out")
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_rotate_sum_hoisted_workspace(self._ptr, batch))
+        n_arr = max(count, 1)
+        g_arr = (ctypes.c_uint32 * n_arr)(*elts)
+        b_arr = (ctypes.c_void_p * n_arr)(*[k[0].data_ptr() if k else None for k in rot_keys])
+        a_arr = (ctypes.c_void_p * n_arr)(*[k[1].data_ptr() if k else None for k in rot_keys])
+        p_arr = (ctypes.c_void_p * n_arr)(*[p.data_ptr() for p in pts])
+        with torch.cuda.device(self.device):
+            check(lib.fhe_rotate_sum_hoisted(self._ptr, _ptr(out), _ptr(ct), g_arr, b_arr, a_arr,
+                                             p_arr, count, batch, _ptr(ws), _stream(ct)),
+                  "fhe_rotate_sum_hoisted")
+        return out
+
     # ---- SURVEY.md §8(f) row 3: sampling, keys, encryption --------------------------------
     # seed=None draws a fresh 64-bit nonce from the OS CSPRNG.  An explicit seed is for
     # reproducible tests: never reuse one per secret key (fhecore.h SECURITY note).

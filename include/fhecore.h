@@ -304,6 +304,22 @@ int fhe_rotate_hoisted(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in,
                        const uint64_t* const* rot_a, uint32_t count, uint32_t batch,
                        void* workspace, fhe_stream_t stream);
 
+/* fhe_rotate_sum_hoisted: out = sum_r pt[r] * rot_{galois_elts[r]}(in) over `count` (1..16)
+ * terms -- the inner loop of a baby-step / giant-step linear transform (CKKS bootstrapping's
+ * CoeffToSlot / SlotToCoeff) -- with one ModUp of c1 and ONE ModDown per output polynomial
+ * (double hoisting: each rotation's key-switch accumulators are multiplied by pt[r] and summed in
+ * the extended basis Q u P before ModDown).  in, out [batch][2][L][N] NTT form over Q (out must
+ * not overlap in); pt[r] [L + K][N] NTT form over Q u P (the diagonal, encoded over the extended
+ * basis); galois_elts[r] == 1 is the unrotated term and takes no key (rot_b[r] / rot_a[r] may be
+ * null there).  Decrypts to sum_r pt_r sigma_r(m) up to one ModDown's rounding; not bit-identical
+ * to summing fhe_rotate_hoisted outputs.  Restated by oracle/pyoracle.py rotate_sum_hoisted.
+ * Contexts with dnum <= 8. */
+size_t fhe_rotate_sum_hoisted_workspace(const fhe_ctx* ctx, uint32_t batch);
+int fhe_rotate_sum_hoisted(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in,
+                           const uint32_t* galois_elts, const uint64_t* const* rot_b,
+                           const uint64_t* const* rot_a, const uint64_t* const* pt,
+                           uint32_t count, uint32_t batch, void* workspace, fhe_stream_t stream);
+
 /* ---- wire format (not in the reference) ------------------------------
  * A self-describing little-endian blob for any [polys][nlimbs][N] residue tensor over context
  * limbs [limb0, limb0 + nlimbs) -- ciphertexts, keys, plaintexts: "FHEC", version 1, flags (bit 0

@@ -73,6 +73,9 @@ def test_errors_are_reported_not_raised():
     # a null key pointer inside the hoisted rotation's key arrays is refused before
     # anything reaches the device (a context is needed first, so only the null context here)
     assert lib.fhe_rotate_hoisted(None, None, None, None, None, None, 1, 1, None, None) == -1
+    assert lib.fhe_rotate_sum_hoisted(None, None, None, None, None, None, None, 1, 1, None,
+                                      None) == -1
+    assert lib.fhe_rotate_sum_hoisted_workspace(None, 1) == 0
 
 
 def test_ctx_create_validates_moduli_before_touching_a_device():
