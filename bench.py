@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch", "mulrelin", "ntt-batch",
-                                           "vec", "rotate"],
+                                           "vec", "rotate", "rotsum"],
                     default="hommult")
     ap.add_argument("--batch", type=int, default=None,
                     help="ciphertexts per GPU per step (default 64 for hommult -- the throughput "
@@ -1271,6 +1271,74 @@ def cpu_baseline_rotate(moduli, special, log_n, dnum, budget_s):
                       f"key-switch, OpenMP {cpu_threads()} threads, in {dt:.1f} s"}
 
 
+def run_rotsum(args, world, rank):
+    """Double-hoisted rotation sum (fhe_rotate_sum_hoisted, the inner loop of a baby-step /
+    giant-step linear transform, a widening beyond SURVEY §8f rows 1 and 4): out = sum_r pt_r
+    rot_r(ct) over R = 8 terms (the unrotated one and 7 rotations) with one ModUp and one ModDown,
+    at the key-switch configuration (N = 2^16, L = 16, K = 4, dnum = 4), batch B per call.
+    `value` counts terms (B R per step).  The same sum through the single-hoisted API
+    (fhe_rotate_hoisted of the 7 rotations, then a plaintext product per term and the adds,
+    fhe_vec_mul / fhe_vec_add) is timed beside it."""
+    L, K, dnum, R = 16, 4, 4, 8
+    n = 1 << args.log_n
+    ctx = fc.Context(args.log_n, L=L, K=K, dnum=dnum)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(17 + rank)
+    B = args.batch
+    ct = uniform_limbs(gen, ctx.moduli, (B, 2), n)
+    elts = [1] + [ctx.galois_elt(r) for r in range(1, R)]
+    keys = [None] + [(uniform_limbs(gen, ctx.all_moduli, (dnum,), n),
+                      uniform_limbs(gen, ctx.all_moduli, (dnum,), n)) for _ in range(R - 1)]
+    pts = [uniform_limbs(gen, ctx.all_moduli, (), n) for _ in range(R)]
+    lib = load()
+    ws = ctx.workspace(max(lib.fhe_rotate_sum_hoisted_workspace(ctx.handle, B),
+                           lib.fhe_rotate_hoisted_workspace(ctx.handle, B)))
+    out = torch.empty(B, 2, L, n, dtype=torch.int64, device="cuda")
+    fused = lambda: ctx.rotate_sum_hoisted(ct, elts, keys, pts, workspace=ws, out=out)  # noqa: E731
+    # the single-hoisted composition: the plaintexts broadcast over the batch (Q rows only)
+    rot = torch.empty(R - 1, B, 2, L, n, dtype=torch.int64, device="cuda")
+    ptq = [p[:L].expand(B, 2, L, n).contiguous() for p in pts]
+    prod = torch.empty(B, 2, L, n, dtype=torch.int64, device="cuda")
+    acc = torch.empty(B, 2, L, n, dtype=torch.int64, device="cuda")
+
+    def single():
+        ctx.rotate_hoisted(ct, elts[1:], keys[1:], workspace=ws, out=rot)
+        ctx.vec("mul", ct, ptq[0], out=acc)
+        for r in range(1, R):
+            ctx.vec("mul", rot[r - 1], ptq[r], out=prod)
+            ctx.vec("add", acc, prod, out=acc)
+
+    dt, kavg = timed(fused, args, world, 64)
+    dt_single, _ = timed(single, args, world, 1)
+    del rot, ptq, prod, acc
+    per_s = B * R * args.steps * world / dt
+    # per call: read the batch's cts (2 L limbs each) and write the sums (2 L), every key
+    # ((R - 1) dnum 2 (L + K) limbs) and plaintext (R (L + K)) once per batch
+    alg_call = (B * 4 * L + (R - 1) * dnum * 2 * (L + K) + R * (L + K)) * n * 8
+    return {"metric": "rotation-sum terms/sec at N=2^16, L=16, K=4, dnum=4 (8 terms per ModUp "
+                      "and per ModDown, double hoisting)",
+            "value": round(per_s, 2), "unit": "terms/s",
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "config": {"workload": "double-hoisted rotation sum (fhe_rotate_sum_hoisted)",
+                       "log_n": args.log_n, "L": L, "K": K, "dnum": dnum, "terms": R,
+                       "rotations": R - 1, "batch": B, "parallelism": f"replicas x{world}"},
+            "rotsums_per_sec": round(B * args.steps * world / dt, 2),
+            "single_hoisted_terms_per_sec": round(B * R * args.steps * world / dt_single, 2),
+            "double_hoisting_speedup": round(dt_single / dt, 3),
+            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
+            "roofline": roofline("rotation sum (whole call, per GPU)", alg_call,
+                                 dt / (args.steps) * 1e3, {"log_n": args.log_n, "L": L, "R": R,
+                                                           "B": B}),
+            # the gathered inner product x plaintext: reads the ModUp digits ((dnum - 1) B (L + K)
+            # rows) and the ct (2 L rows per ciphertext) once per term through the automorphism,
+            # each term's keys and plaintext once, writes the two accumulators and the c0 sums
+            "roofline_rot_sum": roofline(
+                "rot_sum (gathered inner products x plaintexts, per launch)",
+                (R * ((dnum - 1) * B * (L + K) + B * 2 * L + 2 * dnum * (L + K) + (L + K)) +
+                 2 * B * (L + K) + 2 * B * L) * n * 8,
+                kavg.get("rot_sum", float("nan")), {"log_n": args.log_n, "L": L, "B": B})}, None
+
+
 def shard_mismatches(got, ref_full, shard) -> int:
     """Words of this rank's limb slice `got` [..., nlimbs, N] that differ from its limbs of the
     single-device result `ref_full` [..., L, N]."""
@@ -1457,11 +1525,13 @@ def main():
     if args.batch is None:
         # mul-relin and rotate at the key-switch's best batch (32: profiles/r04_ks_batch_sweep.txt,
         # r04_mulrelin_rotate_batch_ab.txt: +2 % / +4 % over 16)
-        args.batch = {"hommult": 64, "mulrelin": 32, "rotate": 32}.get(args.workload, 16)
+        args.batch = {"hommult": 64, "mulrelin": 32, "rotate": 32, "rotsum": 32}.get(
+            args.workload, 16)
     world, rank = dist_setup(args)
     _EMIT.update(json_fd=json_fd, args=args, world=world)
     run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch, "vec": run_vec,
-           "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch, "rotate": run_rotate}[args.workload]
+           "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch, "rotate": run_rotate,
+           "rotsum": run_rotsum}[args.workload]
     out, cpu = run(args, world, rank)
     rc = conclude(out, cpu, rank)
     if world > 1:
