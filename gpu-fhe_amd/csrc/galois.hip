@@ -150,8 +150,21 @@ __device__ __forceinline__ u64 rs_fin(u128 a, const ModParams& m) {
   if constexpr (WIDE) return (u64)a;
   return reduce128((u64)a, (u64)(a >> 64), m);
 }
+// a + x y for x, y < 2^61 by the hand-written 61-bit product (mul_wide61: 4 mads where the
+// compiler's u128 product takes 11 VALU with its register-pair moves)
+__device__ __forceinline__ void rs_mac61(u128& a, u64 x, u64 y) {
+  u64 lo, hi;
+  mul_wide61(x, y, lo, hi);
+  a += ((u128)hi << 64) | lo;
+}
 
-template <int DNUM, bool WIDE>
+// FAST (every modulus < 2^60, the lz16 contexts, and dnum <= 4): each term's inner product is a
+// 128-bit sum on 32-bit halves (dot_wide61) reduced by one Montgomery REDC to t R^-1 in (0, 2q);
+// the term's plaintext word enters as p R mod q (one Shoup product by R per term and position,
+// shared by the kRotSumBC ciphertexts), so (p R)(t R^-1) = p t adds into the 128-bit sums with
+// one mul_wide61 (operands below 2q < 2^61; 16 terms of 4 q^2 stay below 2^126).  Against the u128
+// form: 2 x 4 u128 products and 2 reduce128 per term and ciphertext become 2 dot_wide61 + 2 REDC.
+template <int DNUM, bool WIDE, bool FAST = false>
 __global__ __launch_bounds__(kThreads) void k_rot_sum(u64* __restrict__ acc, u64 acc_ws,
                                                       u64* __restrict__ cadd, int ident,
                                                       const u64* __restrict__ ext,
@@ -181,8 +194,13 @@ __global__ __launch_bounds__(kThreads) void k_rot_sum(u64* __restrict__ acc, u64
         for (u32 bb = 0; bb < kRotSumBC; ++bb) {
           if (bb >= nb) break;
           const u64* ct = in + (u64)(b0 + bb) * 2 * ln + e;
-          rs_mac<WIDE>(a0[bb], p, ct[0], m);
-          rs_mac<WIDE>(a1[bb], p, ct[ln], m);
+          if constexpr (FAST) {
+            rs_mac61(a0[bb], p, ct[0]);
+            rs_mac61(a1[bb], p, ct[ln]);
+          } else {
+            rs_mac<WIDE>(a0[bb], p, ct[0], m);
+            rs_mac<WIDE>(a1[bb], p, ct[ln], m);
+          }
         }
       }
       continue;
@@ -195,6 +213,28 @@ __global__ __launch_bounds__(kThreads) void k_rot_sum(u64* __restrict__ acc, u64
     for (int j = 0; j < DNUM; ++j) {
       kb[j] = tm.kb[k][(u64)j * rn + e];
       ka[j] = tm.ka[k][(u64)j * rn + e];
+    }
+    if constexpr (FAST) {
+      static_assert(!WIDE && DNUM <= 4, "FAST: narrow moduli, dot_wide61 of <= 4 terms");
+      u64 pr = shoup_q3(p, m.r64, m.r64s, 0 - m.q);  // p R mod q in [0, 3q)
+      pr = csub_fast(pr, 0 - 2 * m.q);                 // [0, 2q)
+      const u64 qi = 0 - m.qinv;                       // q^-1 mod 2^64 (mont_redc_x)
+#pragma unroll
+      for (u32 bb = 0; bb < kRotSumBC; ++bb) {
+        if (bb >= nb) break;
+        const u32 b = b0 + bb;
+        u64 x[DNUM];
+#pragma unroll
+        for (int j = 0; j < DNUM; ++j)
+          x[j] = (u32)j == own ? in[(u64)b * 2 * ln + ln + es] : ext[((u64)j * batch + b) * rn + es];
+        u64 lo, hi;
+        dot_wide61<DNUM>(x, kb, lo, hi);
+        rs_mac61(s0[bb], pr, mont_redc_x(lo, hi, m.q, qi));
+        dot_wide61<DNUM>(x, ka, lo, hi);
+        rs_mac61(s1[bb], pr, mont_redc_x(lo, hi, m.q, qi));
+        if (r < L) rs_mac61(a0[bb], p, in[(u64)b * 2 * ln + es]);
+      }
+      continue;
     }
 #pragma unroll
     for (u32 bb = 0; bb < kRotSumBC; ++bb) {
@@ -514,6 +554,9 @@ int launch_rotate_sum_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u
       k_rot_sum<d, true><<<dim3((u32)grid), kThreads, 0, s>>>(acc, acc_ws, cadd, ident, ext, in, \
                                                                tm, rows, L, c->alpha, batch,      \
                                                                c->log_n, c->d_mods);              \
+    else if (c->lz16 && d <= 4)                                                                   \
+      k_rot_sum<(d <= 4 ? d : 4), false, true><<<dim3((u32)grid), kThreads, 0, s>>>(              \
+          acc, acc_ws, cadd, ident, ext, in, tm, rows, L, c->alpha, batch, c->log_n, c->d_mods);  \
     else                                                                                          \
       k_rot_sum<d, false><<<dim3((u32)grid), kThreads, 0, s>>>(                                   \
           acc, acc_ws, cadd, ident, ext, in, tm, rows, L, c->alpha, batch, c->log_n, c->d_mods);  \
