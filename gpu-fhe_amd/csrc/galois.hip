@@ -448,8 +448,14 @@ int launch_rotate_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u32* 
   FHE_HIP_CHECK(hipMemcpy2DAsync(c1, ln * sizeof(u64), in + ln, 2 * ln * sizeof(u64),
                                  ln * sizeof(u64), batch, hipMemcpyDeviceToDevice, s));
   int rc;
-  if ((rc = launch_ntt_strided(c, false, c1, ln, c_all, ln, batch, 0, L, s))) return rc;
-  const CAll call = CAll::contiguous(c_all, L, n);
+  // prepared INTT (the ModUp digits' (D^_k)^-1 folded in) where the hoisted ModUp takes the fused
+  // conversion pass (rns.hip hoist_up)
+  const bool prep = ks_prepared(c);
+  if ((rc = launch_ntt_strided(c, false, c1, ln, c_all, ln, batch, 0, L, s,
+                               prep ? c->d_nfold_up : nullptr, prep && ks_split30(c))))
+    return rc;
+  CAll call = CAll::contiguous(c_all, L, n);
+  call.scaled = prep;
   KsHoist up;
   up.modup_only = true;
   if ((rc = launch_keyswitch_shard(c, nullptr, nullptr, call, c1, nullptr, nullptr, 0, L, batch,
@@ -536,11 +542,16 @@ int launch_rotate_sum_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u
   if (int rc = check_grid(grid, kThreads, 1, 1, "rotate_sum_hoisted")) return rc;
   int rc;
   const CAll call = CAll::contiguous(c_all, L, n);
+  const bool prep = ks_prepared(c);  // the prepared INTT for the fused hoisted ModUp
   if (rotated) {
-    if ((rc = launch_ntt_strided(c, false, in + ln, 2 * ln, c_all, ln, batch, 0, L, s))) return rc;
+    if ((rc = launch_ntt_strided(c, false, in + ln, 2 * ln, c_all, ln, batch, 0, L, s,
+                                 prep ? c->d_nfold_up : nullptr, prep && ks_split30(c))))
+      return rc;
+    CAll callp = call;
+    callp.scaled = prep;
     KsHoist up;
     up.modup_only = true;
-    if ((rc = launch_keyswitch_shard(c, nullptr, nullptr, call, in + ln, nullptr, nullptr, 0, L,
+    if ((rc = launch_keyswitch_shard(c, nullptr, nullptr, callp, in + ln, nullptr, nullptr, 0, L,
                                      batch, kws, s, nullptr, &up)))
       return rc;
   }

@@ -142,6 +142,9 @@ int launch_ntt_col_inv(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst,
 // finishes it).
 int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
                        u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
+// the row-forward pass after k_modup_col (input range scheduled from 2), canonical outputs
+int launch_ntt_row_fwd_r2(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
+                          u32 polys, u32 limb0, u32 nlimbs, hipStream_t s);
 // Fused key-switch row kernel (ntt.hip, k_ks_row_inner): row-forward NTT of every ModUp digit's
 // column-passed rows + inner product with the key.  ext [dnum][batch][rows][N] (digit stride
 // ext_ds words), d2_own [batch][nq][N] NTT form, evk [dnum][rows][N], acc [2][batch][rows][N]

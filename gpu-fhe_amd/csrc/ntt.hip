@@ -898,7 +898,7 @@ __global__ __launch_bounds__(kColThreads) __attribute__((amdgpu_waves_per_eu(4, 
 // One row tile (poly p, limb l, tile) of a row pass (the body of k_ntt_row; lds: G::LDS_R words).
 // The forward stores its last round in linear order through the LDS (XOUT); the inverse loads its
 // first round that way.
-template <int LOGN, bool FWD, int H, bool NTL, bool NTS>
+template <int LOGN, bool FWD, int H, bool NTL, bool NTS, int R0 = 1>
 __device__ __forceinline__ void row_tile(u64* lds, const u64* __restrict__ src,
                                          u64* __restrict__ dst, u32 limb0, const PolyMap& pm,
                                          u32 p, u32 l, u32 tile,
@@ -932,7 +932,7 @@ __device__ __forceinline__ void row_tile(u64* lds, const u64* __restrict__ src,
   } else {
     pass_load<G::N2, FWD>(gin, t, x);
   }
-  pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, H, fwd_range(1, G::N1, H),
+  pass_run<G::N2, FWD, FWD ? kFinalFwd : kNotFinal, kWaveSync, true, H, fwd_range(R0, G::N1, H),
            FWD>(x, GView<1, false, NTS>{dst + pm.dst(p) + loc, lane}, lv, t,
                 tw_all + (u64)limb * N, (u32)G::R1 + row0 + sub, mods[limb].q, {0, 0}, {0, 0});
 }
@@ -941,7 +941,9 @@ __device__ __forceinline__ void row_tile(u64* lds, const u64* __restrict__ src,
 // in that XCD's L2) and the tile varies fastest, so an XCD streams each poly-limb's rows front to
 // back.  (Poly fastest, which re-read a row's twiddles sooner: row passes 8 % slower,
 // profiles/r03_row_order_ab.txt.)
-template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false>
+// R0: the input range (units of q) the preceding column pass was scheduled from (fwd_range); 2 after
+// k_modup_col (the hoisted ModUp's row pass, launch_ntt_row_fwd_r2)
+template <int LOGN, bool FWD, int H = 8, bool NTL = false, bool NTS = false, int R0 = 1>
 __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src, u64* __restrict__ dst, u32 nlimbs,
                                     u32 limb0, PolyMap pm, u32 items,
                                     const ulonglong2* __restrict__ tw_all,
@@ -952,7 +954,7 @@ __global__ FHE_KATTR void k_ntt_row(const u64* __restrict__ src, u64* __restrict
   if (it >= items) return;
   u32 l, rest;
   xcd_limb_split(it, nlimbs, items / nlimbs, l, rest);
-  row_tile<LOGN, FWD, H, NTL, NTS>(lds, src, dst, limb0, pm, rest / G::TILES_R, l,
+  row_tile<LOGN, FWD, H, NTL, NTS, R0>(lds, src, dst, limb0, pm, rest / G::TILES_R, l,
                                    rest % G::TILES_R, tw_all, mods);
 }
 
@@ -2209,6 +2211,36 @@ int launch_ntt_col_fwd(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst,
       return rc;                                                                             \
     FHE_HIP_CHECK(hipGetLastError());                                                       \
     return kOk;
+    FHE_LOGN_CASES(X)
+#undef X
+  }
+  set_error("unsupported log_n");
+  return kUnsupported;
+}
+
+// The row-forward pass over rows that k_modup_col column-passed (its schedule starts from 2):
+// canonical NTT-form outputs, in place or out of place.  The hoisted ModUp (rotations, rotation sums)
+// runs it over each digit's extended rows.
+int launch_ntt_row_fwd_r2(const fhe_ctx* c, const u64* src, u64 spstride, u64* dst, u64 dpstride,
+                          u32 polys, u32 limb0, u32 nlimbs, hipStream_t s) {
+  if ((u64)polys * nlimbs == 0) return kOk;
+  if (c->wide) return wide_unsupported();
+  switch (c->log_n) {
+#define X(n)                                                                                      \
+  case n: {                                                                                       \
+    using G = Geo<n>;                                                                             \
+    const u64 ir = (u64)polys * nlimbs * G::TILES_R;                                              \
+    if (int rc = check_grid(item_blocks(ir), G::THR_R, 1, 1, "ntt_row_fwd")) return rc;           \
+    const PolyMap pm{1, spstride, 0, dpstride, 0, 0};                                             \
+    if (c->lz16)                                                                                  \
+      k_ntt_row<n, true, 16, false, false, 2><<<item_grid(ir), G::THR_R, 0, s>>>(                 \
+          src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_fwd, c->d_mods);                          \
+    else                                                                                          \
+      k_ntt_row<n, true, 8, false, false, 2><<<item_grid(ir), G::THR_R, 0, s>>>(                  \
+          src, dst, nlimbs, limb0, pm, (u32)ir, c->d_tw_fwd, c->d_mods);                          \
+    FHE_HIP_CHECK(hipGetLastError());                                                             \
+    return kOk;                                                                                   \
+  }
     FHE_LOGN_CASES(X)
 #undef X
   }

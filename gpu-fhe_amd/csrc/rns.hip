@@ -458,14 +458,19 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
   // HBM so that each rotation's inner product can gather them through its automorphism.
   const bool fused = !hoist && ks_fused(c);
   const u32 gal = hoist ? hoist->galois : 0;
+  // The hoisted ModUp (modup_only) on the contexts the fused ModUp serves: the same conversion
+  // column pass (plain table: the gathered inner products read plain residues), then one
+  // row-forward pass per digit range (launch_ntt_row_fwd_r2), so the NTT-form digits land in HBM
+  // for the gathers; in place of k_baseconv + a full NTT per range.
+  const bool hoist_up = hoist && hoist->modup_only && ks_prepared(c);
   // Fused ModUp (with the fused row kernel, digits of <= 4 limbs): the base conversion runs
   // inside the column-forward pass (ntt.hip k_modup_col) after a one-pass prologue that scales the
   // digit's source rows; the extended rows are never written in coefficient form.
-  const bool fused_up = fused && alpha <= 4;
+  const bool fused_up = (fused && alpha <= 4) || hoist_up;
   // lz16 fused ModUp: the extended rows come out times R = 2^64 (d_modup_hat_rw / _rwp), which the fused
   // row kernel's Montgomery inner product cancels (KsRowArgs::mont)
-  const bool mont_ext = fused_up && c->lz16;
-  if (call.scaled && !fused_up) {
+  const bool mont_ext = fused_up && !hoist_up && c->lz16;
+  if (call.scaled && !fused_up && (!hoist || hoist->modup_only)) {
     set_error("keyswitch: a prepared (pre-scaled) input needs the fused ModUp (ks_prepared)");
     return kInvalid;
   }
@@ -547,6 +552,23 @@ int launch_keyswitch_shard(const fhe_ctx* c, u64* ks0, u64* ks1, const CAll& cal
     if ((rc = ntt_fwd(e + (u64)nlimbs * n, L, K))) return rc;
   }
   if (npend && (rc = launch_modup_cols(c, pend, npend, s))) return rc;
+  if (hoist_up) {
+    // the row-forward passes of every digit's extended rows: [0, lo) and [hi, rows), whose limbs
+    // are [limb0, limb0 + lo) and (the own Q-limbs past the digit, then P) [hi, L + K) when this
+    // is the single-device form (limb0 = 0, nlimbs = L)
+    for (u32 j = 0; j < c->dnum; ++j) {
+      const u32 lo = j * alpha, hi = std::min(L, lo + alpha);
+      u64* e = ext + (u64)j * B * rn;
+      if (limb0 != 0 || nlimbs != L) {
+        set_error("keyswitch: the hoisted ModUp is single-device (all Q-limbs)");
+        return kInvalid;
+      }
+      if ((rc = launch_ntt_row_fwd_r2(c, e, rn, e, rn, batch, 0, lo, s)) ||
+          (rc = launch_ntt_row_fwd_r2(c, e + (u64)hi * n, rn, e + (u64)hi * n, rn, batch, hi,
+                                      rows - hi, s)))
+        return rc;
+    }
+  }
   prof_mark(s, "ks_modup");
   if (hoist) return kOk;  // modup_only: the NTT-form digits stay in the workspace's ext region
   }
