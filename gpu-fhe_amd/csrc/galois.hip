@@ -132,7 +132,10 @@ struct RotSumTerms {
   const u64* ka[kRotSumMax];
   const u64* pt[kRotSumMax];
 };
-constexpr u32 kRotSumBC = 4;
+// 2 ciphertexts per thread: 110 VGPRs, 4 waves per SIMD for the gathers' latency; 4 took 182 (2
+// waves): rot_sum 3.30 -> 2.48 ms per 32 x 8 terms, +18 % terms/s same-box
+// (profiles/r06_rotsum_bc_ab.txt)
+constexpr u32 kRotSumBC = 2;
 
 // a + x y for the rotation sum's 128-bit accumulators: narrow moduli (q < 2^61) add exact
 // products (at most 16 terms of q^2 < 2^122 each); wide ones reduce every product
