@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", choices=["hommult", "ntt", "keyswitch", "mulrelin", "ntt-batch",
-                                           "vec", "rotate", "rotsum"],
+                                           "vec", "rotate", "rotsum", "lintrans"],
                     default="hommult")
     ap.add_argument("--batch", type=int, default=None,
                     help="ciphertexts per GPU per step (default 64 for hommult -- the throughput "
@@ -1339,6 +1339,72 @@ def run_rotsum(args, world, rank):
                 kavg.get("rot_sum", float("nan")), {"log_n": args.log_n, "L": L, "B": B})}, None
 
 
+def run_lintrans(args, world, rank):
+    """Baby-step / giant-step linear transform with both hoistings (fhe_linear_transform: CKKS
+    bootstrapping's CoeffToSlot / SlotToCoeff shape, a widening beyond SURVEY §8f rows 1 and 4):
+    n1 = 4 baby x n2 = 4 giant steps = 16 diagonals per ciphertext, at the key-switch configuration
+    (N = 2^16, L = 16, K = 4, dnum = 4), batch B per call.  `value` counts transforms (B per step).
+    The same 16-diagonal product by the hoisted diagonal method (fhe_rotate_hoisted of the 15
+    rotations, then a plaintext product per diagonal and the adds) is timed beside it."""
+    L, K, dnum, n1, n2 = 16, 4, 4, 4, 4
+    n = 1 << args.log_n
+    ctx = fc.Context(args.log_n, L=L, K=K, dnum=dnum)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(19 + rank)
+    B = args.batch
+    ct = uniform_limbs(gen, ctx.moduli, (B, 2), n)
+    key = lambda: (uniform_limbs(gen, ctx.all_moduli, (dnum,), n),  # noqa: E731
+                   uniform_limbs(gen, ctx.all_moduli, (dnum,), n))
+    baby = [1] + [ctx.galois_elt(b) for b in range(1, n1)]
+    giant = [1] + [ctx.galois_elt(g * n1) for g in range(1, n2)]
+    bkeys = [None] + [key() for _ in range(1, n1)]
+    gkeys = [None] + [key() for _ in range(1, n2)]
+    pts = [[uniform_limbs(gen, ctx.all_moduli, (), n) for _ in range(n1)] for _ in range(n2)]
+    lib = load()
+    ws = ctx.workspace(max(lib.fhe_linear_transform_workspace(ctx.handle, n2, B),
+                           lib.fhe_rotate_hoisted_workspace(ctx.handle, B)))
+    out = torch.empty(B, 2, L, n, dtype=torch.int64, device="cuda")
+    fused = lambda: ctx.linear_transform(ct, baby, bkeys, giant, gkeys, pts, workspace=ws,  # noqa: E731
+                                         out=out)
+    dt, kavg = timed(fused, args, world, 128)
+    # the hoisted diagonal method: sum_i diag_i rot_i(ct), i < n1 n2, one ModUp for the rotations
+    D = n1 * n2
+    elts = [ctx.galois_elt(i) for i in range(1, D)]
+    keys = [key() for _ in range(1, D)]
+    rot = torch.empty(D - 1, B, 2, L, n, dtype=torch.int64, device="cuda")
+    diag = [uniform_limbs(gen, ctx.moduli, (), n).expand(B, 2, L, n).contiguous()
+            for _ in range(D)]
+    prod = torch.empty(B, 2, L, n, dtype=torch.int64, device="cuda")
+    acc = torch.empty(B, 2, L, n, dtype=torch.int64, device="cuda")
+
+    def diagonal():
+        ctx.rotate_hoisted(ct, elts, keys, workspace=ws, out=rot)
+        ctx.vec("mul", ct, diag[0], out=acc)
+        for i in range(1, D):
+            ctx.vec("mul", rot[i - 1], diag[i], out=prod)
+            ctx.vec("add", acc, prod, out=acc)
+
+    dt_diag, _ = timed(diagonal, args, world, 1)
+    del rot, diag, prod, acc
+    per_s = B * args.steps * world / dt
+    # per call: read the cts (2 L limbs each), write the results (2 L); every key ((n1 - 1) +
+    # (n2 - 1) rotation keys of dnum 2 (L + K) limbs) and diagonal (n1 n2 (L + K)) once per batch
+    alg_call = (B * 4 * L + (n1 + n2 - 2) * dnum * 2 * (L + K) + D * (L + K)) * n * 8
+    return {"metric": "BSGS linear transforms/sec at N=2^16, L=16, K=4, dnum=4 (16 diagonals: "
+                      "4 baby x 4 giant steps, double hoisting)",
+            "value": round(per_s, 2), "unit": "transforms/s",
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "config": {"workload": "BSGS linear transform (fhe_linear_transform)",
+                       "log_n": args.log_n, "L": L, "K": K, "dnum": dnum, "n1": n1, "n2": n2,
+                       "diagonals": D, "batch": B, "parallelism": f"replicas x{world}"},
+            "diagonals_per_sec": round(D * per_s, 2),
+            "hoisted_diagonal_method_per_sec": round(B * args.steps * world / dt_diag, 2),
+            "bsgs_speedup": round(dt_diag / dt, 3),
+            "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
+            "roofline": roofline("linear transform (whole call, per GPU)", alg_call,
+                                 dt / args.steps * 1e3, {"log_n": args.log_n, "L": L, "B": B})}, None
+
+
 def shard_mismatches(got, ref_full, shard) -> int:
     """Words of this rank's limb slice `got` [..., nlimbs, N] that differ from its limbs of the
     single-device result `ref_full` [..., L, N]."""
@@ -1525,13 +1591,14 @@ def main():
     if args.batch is None:
         # mul-relin and rotate at the key-switch's best batch (32: profiles/r04_ks_batch_sweep.txt,
         # r04_mulrelin_rotate_batch_ab.txt: +2 % / +4 % over 16)
-        args.batch = {"hommult": 64, "mulrelin": 32, "rotate": 32, "rotsum": 32}.get(
+        args.batch = {"hommult": 64, "mulrelin": 32, "rotate": 32, "rotsum": 32,
+                      "lintrans": 32}.get(
             args.workload, 16)
     world, rank = dist_setup(args)
     _EMIT.update(json_fd=json_fd, args=args, world=world)
     run = {"hommult": run_hommult, "ntt": run_ntt, "keyswitch": run_keyswitch, "vec": run_vec,
            "mulrelin": run_mulrelin, "ntt-batch": run_ntt_batch, "rotate": run_rotate,
-           "rotsum": run_rotsum}[args.workload]
+           "rotsum": run_rotsum, "lintrans": run_lintrans}[args.workload]
     out, cpu = run(args, world, rank)
     rc = conclude(out, cpu, rank)
     if world > 1:

@@ -439,6 +439,85 @@ int fhe_rotate_sum_hoisted(const fhe_ctx* c, uint64_t* out, const uint64_t* in,
                                    hs(s));
 }
 
+size_t fhe_rotate_sum_multi_workspace(const fhe_ctx* c, uint32_t batch) {
+  return c ? rotate_sum_multi_workspace_bytes(c, batch) : 0;
+}
+
+int fhe_rotate_sum_multi(const fhe_ctx* c, uint64_t* out, const uint64_t* const* cts,
+                         const uint32_t* galois_elts, const uint64_t* const* rot_b,
+                         const uint64_t* const* rot_a, uint32_t count, uint32_t batch, void* ws,
+                         fhe_stream_t s) {
+  int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_rotate_sum_multi");
+  if (rc) return rc;
+  if (count == 0 || count > kRotSumMax) {
+    set_error("fhe_rotate_sum_multi: count must be 1..16");
+    return kInvalid;
+  }
+  if (!galois_elts || !cts || ((!rot_b || !rot_a) && std::any_of(galois_elts, galois_elts + count,
+                                                                  [](uint32_t g) { return g != 1; }))) {
+    set_error("fhe_rotate_sum_multi: null Galois element, ciphertext or key array");
+    return kInvalid;
+  }
+  const uint64_t span = (uint64_t)batch * 2 * c->L * c->n;
+  for (uint32_t r = 0; r < count; ++r) {
+    if (!cts[r] || (galois_elts[r] != 1 && (!rot_b[r] || !rot_a[r]))) {
+      set_error("fhe_rotate_sum_multi: null ciphertext or key pointer for term " +
+                std::to_string(r));
+      return kInvalid;
+    }
+    if (spans_overlap(out, span, cts[r], span)) {
+      set_error("fhe_rotate_sum_multi: out must not overlap an input ciphertext (term " +
+                std::to_string(r) + ")");
+      return kInvalid;
+    }
+  }
+  if ((rc = ensure_ws(c, rotate_sum_multi_workspace_bytes(c, batch), &ws, hs(s)))) return rc;
+  return launch_rotate_sum_multi(c, out, cts, galois_elts, rot_b, rot_a, count, batch, ws, hs(s));
+}
+
+size_t fhe_linear_transform_workspace(const fhe_ctx* c, uint32_t n2, uint32_t batch) {
+  return c ? linear_transform_workspace_bytes(c, n2, batch) : 0;
+}
+
+int fhe_linear_transform(const fhe_ctx* c, uint64_t* out, const uint64_t* in, uint32_t n1,
+                         uint32_t n2, const uint32_t* baby_elts, const uint64_t* const* baby_b,
+                         const uint64_t* const* baby_a, const uint32_t* giant_elts,
+                         const uint64_t* const* giant_b, const uint64_t* const* giant_a,
+                         const uint64_t* const* pt, uint32_t batch, void* ws, fhe_stream_t s) {
+  int rc = check_window(c, 0, c ? c->L : 0, c ? c->L : 0, "fhe_linear_transform");
+  if (rc) return rc;
+  if (n1 == 0 || n1 > kRotSumMax || n2 == 0 || n2 > kRotSumMax) {
+    set_error("fhe_linear_transform: n1 and n2 must be 1..16");
+    return kInvalid;
+  }
+  if (!baby_elts || !giant_elts || !pt) {
+    set_error("fhe_linear_transform: null Galois element or plaintext array");
+    return kInvalid;
+  }
+  auto keyed = [](const uint32_t* e, uint32_t k, const uint64_t* const* b, const uint64_t* const* a) {
+    for (uint32_t r = 0; r < k; ++r)
+      if (e[r] != 1 && (!b || !a || !b[r] || !a[r])) return false;
+    return true;
+  };
+  if (!keyed(baby_elts, n1, baby_b, baby_a) || !keyed(giant_elts, n2, giant_b, giant_a)) {
+    set_error("fhe_linear_transform: a rotated baby or giant step without its key");
+    return kInvalid;
+  }
+  for (uint64_t r = 0; r < (uint64_t)n1 * n2; ++r)
+    if (!pt[r]) {
+      set_error("fhe_linear_transform: null plaintext pointer " + std::to_string(r));
+      return kInvalid;
+    }
+  const uint64_t span = (uint64_t)batch * 2 * c->L * c->n;
+  if (spans_overlap(out, span, in, span)) {
+    set_error("fhe_linear_transform: out must not overlap in");
+    return kInvalid;
+  }
+  if ((rc = ensure_ws(c, linear_transform_workspace_bytes(c, n2, batch), &ws, hs(s)))) return rc;
+  return launch_linear_transform(c, out, in, n1, n2, baby_elts, baby_b, baby_a, giant_elts, giant_b,
+                                 giant_a, pt, batch, ws, hs(s));
+}
+
 size_t fhe_mul_relin_workspace(const fhe_ctx* c, uint32_t batch) {
   return c ? mul_relin_workspace_bytes(c, batch) : 0;
 }

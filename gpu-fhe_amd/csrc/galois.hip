@@ -136,6 +136,9 @@ struct RotSumTerms {
 // waves): rot_sum 3.30 -> 2.48 ms per 32 x 8 terms, +18 % terms/s same-box
 // (profiles/r06_rotsum_bc_ab.txt)
 constexpr u32 kRotSumBC = 2;
+// k_rot_sum flags: write the unrotated term's c1 sum (cadd's second half); start from the sums in
+// acc / cadd instead of zero (one launch per term of rotate_sum_multi)
+constexpr int kRotSumC1 = 1, kRotSumAccum = 2;
 
 // a + x y for the rotation sum's 128-bit accumulators: narrow moduli (q < 2^61) add exact
 // products (at most 16 terms of q^2 < 2^122 each); wide ones reduce every product
@@ -169,7 +172,7 @@ __device__ __forceinline__ void rs_mac61(u128& a, u64 x, u64 y) {
 // form: 2 x 4 u128 products and 2 reduce128 per term and ciphertext become 2 dot_wide61 + 2 REDC.
 template <int DNUM, bool WIDE, bool FAST = false>
 __global__ __launch_bounds__(kThreads) void k_rot_sum(u64* __restrict__ acc, u64 acc_ws,
-                                                      u64* __restrict__ cadd, int ident,
+                                                      u64* __restrict__ cadd, int flags,
                                                       const u64* __restrict__ ext,
                                                       const u64* __restrict__ in,
                                                       const RotSumTerms tm, u32 rows, u32 L,
@@ -187,10 +190,24 @@ __global__ __launch_bounds__(kThreads) void k_rot_sum(u64* __restrict__ acc, u64
   const u32 own = r < L ? r / alpha : 0xffffffffu;
   const u32 b0 = bc * kRotSumBC, nb = min(kRotSumBC, batch - b0);
   u128 s0[kRotSumBC] = {}, s1[kRotSumBC] = {}, a0[kRotSumBC] = {}, a1[kRotSumBC] = {};
+  const bool ident = (flags & kRotSumC1) != 0;
+  if (flags & kRotSumAccum) {  // add to the sums a previous launch left (canonical words)
+#pragma unroll
+    for (u32 bb = 0; bb < kRotSumBC; ++bb) {
+      if (bb >= nb) break;
+      const u32 b = b0 + bb;
+      s0[bb] = acc[(u64)b * rn + e];
+      s1[bb] = acc[acc_ws + (u64)b * rn + e];
+      if (r < L) {
+        a0[bb] = cadd[(u64)b * ln + e];
+        if (ident) a1[bb] = cadd[(u64)(batch + b) * ln + e];
+      }
+    }
+  }
   const u32 sh = 32 - log_n, mask2 = (2u << log_n) - 1;
   for (u32 k = 0; k < tm.count; ++k) {
     const u32 g = tm.gal[k];
-    const u64 p = tm.pt[k][e];
+    const u64 p = tm.pt[k] ? tm.pt[k][e] : 1;  // no plaintext: the term itself (rotate_sum_multi)
     if (g == 1) {  // the unrotated term (workgroup-uniform)
       if (r < L) {
 #pragma unroll
@@ -495,6 +512,115 @@ size_t rotate_sum_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch) {
          keyswitch_workspace_bytes(c, c->L, batch);
 }
 
+namespace {
+// The rotation sums' workspace regions (rotate_sum_hoisted_workspace_bytes)
+struct RotSumWs {
+  u64* c_all;  // [batch][L][N] coefficient form of the c1 being ModUp'ed
+  u64* cadd;   // [2][batch][L][N]: the c0 sum, then the unrotated terms' c1 sum
+  u64* ydn;    // [2 batch][K][N] the fused ModDown's INTT output
+  u64* kws;    // key-switch workspace: ext [dnum][batch][L + K][N], then the accumulators
+};
+RotSumWs rotsum_ws(const fhe_ctx* c, void* ws, u32 batch) {
+  const u64 ln = (u64)c->L * c->n;
+  RotSumWs w;
+  w.c_all = static_cast<u64*>(ws);
+  w.cadd = w.c_all + batch * ln;
+  w.ydn = w.cadd + 2 * batch * ln;
+  w.kws = w.ydn + 2 * batch * (u64)c->K * c->n;
+  return w;
+}
+
+int rotsum_check(const fhe_ctx* c, u32 count, const u32* galois, const char* who) {
+  if (c->K == 0) {
+    set_error(std::string(who) + ": context has no special primes (K = 0)");
+    return kInvalid;
+  }
+  if (count > kRotSumMax) {
+    set_error(std::string(who) + ": at most 16 terms per call");
+    return kInvalid;
+  }
+  if (c->dnum > 8) {
+    set_error(std::string(who) + ": dnum > 8");
+    return kUnsupported;
+  }
+  const u32 two_n = 2u << c->log_n;
+  for (u32 r = 0; r < count; ++r)
+    if ((galois[r] & 1) == 0 || galois[r] >= two_n) {
+      set_error(std::string(who) + ": every Galois element must be odd and below 2N");
+      return kInvalid;
+    }
+  return kOk;
+}
+
+// ModUp of in's c1 ([batch][2][L][N], NTT form) into the ext region: the prepared INTT (the fused
+// hoisted ModUp's scaled inputs) and the hoisted ModUp (rns.hip, modup_only)
+int rotsum_modup(const fhe_ctx* c, const u64* in, u32 batch, const RotSumWs& w, hipStream_t s) {
+  const u32 L = c->L;
+  const u64 ln = (u64)L * c->n;
+  const bool prep = ks_prepared(c);
+  if (int rc = launch_ntt_strided(c, false, in + ln, 2 * ln, w.c_all, ln, batch, 0, L, s,
+                                  prep ? c->d_nfold_up : nullptr, prep && ks_split30(c)))
+    return rc;
+  CAll call = CAll::contiguous(w.c_all, L, c->n);
+  call.scaled = prep;
+  KsHoist up;
+  up.modup_only = true;
+  return launch_keyswitch_shard(c, nullptr, nullptr, call, in + ln, nullptr, nullptr, 0, L, batch,
+                                w.kws, s, nullptr, &up);
+}
+
+// One k_rot_sum launch over the terms tm of ciphertexts in (whose ModUp is in the ext region when
+// a term is rotated): the accumulators and cadd get the sums (flags: kRotSumC1, kRotSumAccum)
+int rotsum_pass(const fhe_ctx* c, const u64* in, const RotSumTerms& tm, int flags, u32 batch,
+                const RotSumWs& w, hipStream_t s) {
+  const u32 L = c->L, rows = L + c->K;
+  const u64 n = c->n;
+  const u64 blocks = (u64)rows * (n / kThreads);
+  const u64 grid = (blocks + 7) / 8 * 8 * ((batch + kRotSumBC - 1) / kRotSumBC);
+  if (int rc = check_grid(grid, kThreads, 1, 1, "rotate_sum")) return rc;
+  u64* acc = ks_acc_region(c, w.kws, L, batch);
+  const u64 acc_ws = (u64)batch * rows * n;
+  const u64* ext = w.kws;
+  switch (c->dnum) {
+#define X(d)                                                                                      \
+  case d:                                                                                         \
+    if (c->wide)                                                                                  \
+      k_rot_sum<d, true><<<dim3((u32)grid), kThreads, 0, s>>>(                                    \
+          acc, acc_ws, w.cadd, flags, ext, in, tm, rows, L, c->alpha, batch, c->log_n, c->d_mods);\
+    else if (c->lz16 && d <= 4)                                                                   \
+      k_rot_sum<(d <= 4 ? d : 4), false, true><<<dim3((u32)grid), kThreads, 0, s>>>(              \
+          acc, acc_ws, w.cadd, flags, ext, in, tm, rows, L, c->alpha, batch, c->log_n, c->d_mods);\
+    else                                                                                          \
+      k_rot_sum<d, false><<<dim3((u32)grid), kThreads, 0, s>>>(                                   \
+          acc, acc_ws, w.cadd, flags, ext, in, tm, rows, L, c->alpha, batch, c->log_n, c->d_mods);\
+    break;
+    X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+#undef X
+  }
+  FHE_HIP_CHECK(hipGetLastError());
+  prof_mark(s, "rot_sum");
+  return kOk;
+}
+
+// ONE ModDown of both sums into out [batch][2][L][N]; out_0 += the c0 sum, out_1 += the unrotated
+// terms' c1 sum (c1) in its finish
+int rotsum_moddown(const fhe_ctx* c, u64* out, const u64* d2ref, bool c1, u32 batch,
+                   const RotSumWs& w, hipStream_t s) {
+  const u32 L = c->L;
+  const u64 ln = (u64)L * c->n;
+  KsHoist h;
+  h.acc_ready = true;
+  h.ydn = w.ydn;
+  KsEpilogue ep;
+  ep.out_bs = 2 * ln;
+  ep.add0 = w.cadd;
+  ep.add1 = c1 ? w.cadd + batch * ln : nullptr;
+  ep.add_bs = ln;
+  return launch_keyswitch_shard(c, out, out + ln, CAll::contiguous(w.c_all, L, c->n), d2ref,
+                                nullptr, nullptr, 0, L, batch, w.kws, s, &ep, &h);
+}
+}  // namespace
+
 // Double hoisting (the inner loop of a baby-step / giant-step linear transform): ModUp(c1) once
 // (as launch_rotate_hoisted), one k_rot_sum pass that forms every rotation's inner product through
 // its automorphism, multiplies it by pt_r and sums the terms in Q u P, then ONE ModDown per
@@ -505,27 +631,11 @@ int launch_rotate_sum_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u
                               const u64* const* rot_b, const u64* const* rot_a,
                               const u64* const* pt, u32 count, u32 batch, void* ws,
                               hipStream_t s) {
-  if (c->K == 0) {
-    set_error("rotate_sum_hoisted: context has no special primes (K = 0)");
-    return kInvalid;
-  }
-  if (count > kRotSumMax) {
-    set_error("rotate_sum_hoisted: at most 16 terms per call");
-    return kInvalid;
-  }
-  if (c->dnum > 8) {
-    set_error("rotate_sum_hoisted: dnum > 8");
-    return kUnsupported;
-  }
-  const u32 two_n = 2u << c->log_n;
+  if (int rc = rotsum_check(c, count, galois, "rotate_sum_hoisted")) return rc;
   RotSumTerms tm{};
   tm.count = count;
   bool ident = false, rotated = false;
   for (u32 r = 0; r < count; ++r) {
-    if ((galois[r] & 1) == 0 || galois[r] >= two_n) {
-      set_error("rotate_sum_hoisted: every Galois element must be odd and below 2N");
-      return kInvalid;
-    }
     tm.gal[r] = galois[r];
     tm.kb[r] = rot_b[r];
     tm.ka[r] = rot_a[r];
@@ -534,63 +644,94 @@ int launch_rotate_sum_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u
     rotated = rotated || galois[r] != 1;
   }
   if (batch == 0) return kOk;
-  const u32 L = c->L, K = c->K, rows = L + K;
-  const u64 n = c->n, ln = (u64)L * n;
-  u64* c_all = static_cast<u64*>(ws);  // [batch][L][N] coefficient form of c1
-  u64* cadd = c_all + batch * ln;      // [2][batch][L][N]
-  u64* ydn = cadd + 2 * batch * ln;    // [2 batch][K][N]
-  u64* kws = ydn + 2 * batch * (u64)K * n;
-  const u64 blocks = (u64)rows * (n / kThreads);
-  const u64 grid = (blocks + 7) / 8 * 8 * ((batch + kRotSumBC - 1) / kRotSumBC);
-  if (int rc = check_grid(grid, kThreads, 1, 1, "rotate_sum_hoisted")) return rc;
+  const RotSumWs w = rotsum_ws(c, ws, batch);
   int rc;
-  const CAll call = CAll::contiguous(c_all, L, n);
-  const bool prep = ks_prepared(c);  // the prepared INTT for the fused hoisted ModUp
-  if (rotated) {
-    if ((rc = launch_ntt_strided(c, false, in + ln, 2 * ln, c_all, ln, batch, 0, L, s,
-                                 prep ? c->d_nfold_up : nullptr, prep && ks_split30(c))))
-      return rc;
-    CAll callp = call;
-    callp.scaled = prep;
-    KsHoist up;
-    up.modup_only = true;
-    if ((rc = launch_keyswitch_shard(c, nullptr, nullptr, callp, in + ln, nullptr, nullptr, 0, L,
-                                     batch, kws, s, nullptr, &up)))
+  if (rotated && (rc = rotsum_modup(c, in, batch, w, s))) return rc;
+  if ((rc = rotsum_pass(c, in, tm, ident ? kRotSumC1 : 0, batch, w, s))) return rc;
+  return rotsum_moddown(c, out, in + (u64)c->L * c->n, ident, batch, w, s);
+}
+
+size_t rotate_sum_multi_workspace_bytes(const fhe_ctx* c, u32 batch) {
+  return rotate_sum_hoisted_workspace_bytes(c, batch);
+}
+
+// sum_r rot_{galois[r]}(cts[r]) over count DIFFERENT ciphertexts with ONE ModDown (the giant-step
+// sum of a baby-step / giant-step linear transform, Bossuat et al.'s second hoisting): per term a
+// ModUp of its own c1 and one accumulating k_rot_sum pass (no plaintext), then one ModDown of the
+// summed accumulators with the sigma(c0) sum (and the unrotated terms' c0, c1) added in its finish.
+// Restated by oracle/pyoracle.py rotate_sum_multi.
+int launch_rotate_sum_multi(const fhe_ctx* c, u64* out, const u64* const* cts, const u32* galois,
+                            const u64* const* rot_b, const u64* const* rot_a, u32 count,
+                            u32 batch, void* ws, hipStream_t s) {
+  if (int rc = rotsum_check(c, count, galois, "rotate_sum_multi")) return rc;
+  if (batch == 0 || count == 0) return kOk;
+  const RotSumWs w = rotsum_ws(c, ws, batch);
+  for (u32 r = 0; r < count; ++r) {
+    RotSumTerms tm{};
+    tm.count = 1;
+    tm.gal[0] = galois[r];
+    tm.kb[0] = rot_b ? rot_b[r] : nullptr;
+    tm.ka[0] = rot_a ? rot_a[r] : nullptr;
+    tm.pt[0] = nullptr;
+    int rc;
+    if (galois[r] != 1 && (rc = rotsum_modup(c, cts[r], batch, w, s))) return rc;
+    if ((rc = rotsum_pass(c, cts[r], tm, kRotSumC1 | (r > 0 ? kRotSumAccum : 0), batch, w, s)))
       return rc;
   }
-  u64* acc = ks_acc_region(c, kws, L, batch);
-  const u64 acc_ws = (u64)batch * rows * n;
-  const u64* ext = static_cast<const u64*>(kws);
-  switch (c->dnum) {
-#define X(d)                                                                                      \
-  case d:                                                                                         \
-    if (c->wide)                                                                                  \
-      k_rot_sum<d, true><<<dim3((u32)grid), kThreads, 0, s>>>(acc, acc_ws, cadd, ident, ext, in, \
-                                                               tm, rows, L, c->alpha, batch,      \
-                                                               c->log_n, c->d_mods);              \
-    else if (c->lz16 && d <= 4)                                                                   \
-      k_rot_sum<(d <= 4 ? d : 4), false, true><<<dim3((u32)grid), kThreads, 0, s>>>(              \
-          acc, acc_ws, cadd, ident, ext, in, tm, rows, L, c->alpha, batch, c->log_n, c->d_mods);  \
-    else                                                                                          \
-      k_rot_sum<d, false><<<dim3((u32)grid), kThreads, 0, s>>>(                                   \
-          acc, acc_ws, cadd, ident, ext, in, tm, rows, L, c->alpha, batch, c->log_n, c->d_mods);  \
-    break;
-    X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
-#undef X
+  return rotsum_moddown(c, out, cts[0] + (u64)c->L * c->n, true, batch, w, s);
+}
+
+size_t linear_transform_workspace_bytes(const fhe_ctx* c, u32 n2, u32 batch) {
+  // the rotation sums' workspace, then the n2 giant-step inputs [n2][batch][2][L][N]
+  return rotate_sum_hoisted_workspace_bytes(c, batch) +
+         (size_t)n2 * batch * 2 * c->L * c->n * sizeof(u64);
+}
+
+// Baby-step / giant-step linear transform with both hoistings (CKKS bootstrapping's CoeffToSlot /
+// SlotToCoeff shape):  out = sum_g rot_{giant[g]}( sum_b pt[g n1 + b] rot_{baby[b]}(in) ).
+// ONE ModUp of in's c1 serves every baby step of every giant step; each giant step's inner sum is
+// one k_rot_sum pass + one ModDown (as launch_rotate_sum_hoisted, bit for bit); the giant sum is
+// launch_rotate_sum_multi (one ModDown).  Restated by oracle/pyoracle.py linear_transform.
+int launch_linear_transform(const fhe_ctx* c, u64* out, const u64* in, u32 n1, u32 n2,
+                            const u32* baby, const u64* const* baby_b, const u64* const* baby_a,
+                            const u32* giant, const u64* const* giant_b,
+                            const u64* const* giant_a, const u64* const* pt, u32 batch, void* ws,
+                            hipStream_t s) {
+  if (n1 == 0 || n2 == 0 || n1 > kRotSumMax || n2 > kRotSumMax) {
+    set_error("linear_transform: n1 and n2 must be 1..16");
+    return kInvalid;
   }
-  FHE_HIP_CHECK(hipGetLastError());
-  prof_mark(s, "rot_sum");
-  // ModDown of both sums; out_0 += C0, out_1 += C1 (the unrotated term's pt c1) in its finish
-  KsHoist h;
-  h.acc_ready = true;
-  h.ydn = ydn;
-  KsEpilogue ep;
-  ep.out_bs = 2 * ln;
-  ep.add0 = cadd;
-  ep.add1 = ident ? cadd + batch * ln : nullptr;
-  ep.add_bs = ln;
-  return launch_keyswitch_shard(c, out, out + ln, call, in + ln, nullptr, nullptr, 0, L, batch, kws,
-                                s, &ep, &h);
+  if (int rc = rotsum_check(c, n1, baby, "linear_transform")) return rc;
+  if (int rc = rotsum_check(c, n2, giant, "linear_transform")) return rc;
+  if (batch == 0) return kOk;
+  const RotSumWs w = rotsum_ws(c, ws, batch);
+  const u64 ct_words = (u64)batch * 2 * c->L * c->n;
+  u64* inner = reinterpret_cast<u64*>(static_cast<char*>(ws) +
+                                      rotate_sum_hoisted_workspace_bytes(c, batch));
+  bool ident = false, rotated = false;
+  for (u32 b = 0; b < n1; ++b) {
+    ident = ident || baby[b] == 1;
+    rotated = rotated || baby[b] != 1;
+  }
+  int rc;
+  if (rotated && (rc = rotsum_modup(c, in, batch, w, s))) return rc;
+  const u64* inner_ptr[kRotSumMax];
+  for (u32 g = 0; g < n2; ++g) {
+    RotSumTerms tm{};
+    tm.count = n1;
+    for (u32 b = 0; b < n1; ++b) {
+      tm.gal[b] = baby[b];
+      tm.kb[b] = baby_b ? baby_b[b] : nullptr;
+      tm.ka[b] = baby_a ? baby_a[b] : nullptr;
+      tm.pt[b] = pt[(u64)g * n1 + b];
+    }
+    u64* ig = inner + (u64)g * ct_words;
+    if ((rc = rotsum_pass(c, in, tm, ident ? kRotSumC1 : 0, batch, w, s)) ||
+        (rc = rotsum_moddown(c, ig, in + (u64)c->L * c->n, ident, batch, w, s)))
+      return rc;
+    inner_ptr[g] = ig;
+  }
+  return launch_rotate_sum_multi(c, out, inner_ptr, giant, giant_b, giant_a, n2, batch, ws, s);
 }
 
 }  // namespace fhe

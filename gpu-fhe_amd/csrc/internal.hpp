@@ -387,6 +387,18 @@ int launch_rotate_sum_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u
                               const u64* const* pt, u32 count, u32 batch, void* ws,
                               hipStream_t s);
 size_t rotate_sum_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch);
+// sum_r rot_{galois[r]}(cts[r]) over different ciphertexts [batch][2][L][N] with one ModDown
+int launch_rotate_sum_multi(const fhe_ctx* c, u64* out, const u64* const* cts, const u32* galois,
+                            const u64* const* rot_b, const u64* const* rot_a, u32 count,
+                            u32 batch, void* ws, hipStream_t s);
+size_t rotate_sum_multi_workspace_bytes(const fhe_ctx* c, u32 batch);
+// out = sum_g rot_{giant[g]}(sum_b pt[g n1 + b] rot_{baby[b]}(in)), both hoistings
+int launch_linear_transform(const fhe_ctx* c, u64* out, const u64* in, u32 n1, u32 n2,
+                            const u32* baby, const u64* const* baby_b, const u64* const* baby_a,
+                            const u32* giant, const u64* const* giant_b,
+                            const u64* const* giant_a, const u64* const* pt, u32 batch, void* ws,
+                            hipStream_t s);
+size_t linear_transform_workspace_bytes(const fhe_ctx* c, u32 n2, u32 batch);
 
 // ---- launchers (pipeline.hip): SURVEY.md §8(f) row 4 -----------------------------------
 int launch_mul_relin(const fhe_ctx* c, u64* out, const u64* a, const u64* b, const u64* evk_b,

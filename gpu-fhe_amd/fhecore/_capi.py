@@ -78,6 +78,11 @@ SIGNATURES = {
     "fhe_rotate_hoisted": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     "fhe_rotate_sum_hoisted_workspace": (_sz, [_vp, _u32]),
     "fhe_rotate_sum_hoisted": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
+    "fhe_rotate_sum_multi_workspace": (_sz, [_vp, _u32]),
+    "fhe_rotate_sum_multi": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
+    "fhe_linear_transform_workspace": (_sz, [_vp, _u32, _u32]),
+    "fhe_linear_transform": (_i32, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _u32, _vp, _vp]),
     "fhe_serialized_size": (_sz, [_vp, _u32, _u32]),
     "fhe_serialize": (_i32, [_vp, _vp, _u32, _u32, _u32, _i32, _vp, _sz, _vp]),
     "fhe_deserialize": (_i32, [_vp, _vp, _sz, _vp, _sz, ctypes.POINTER(_u32), ctypes.POINTER(_u32),

@@ -430,6 +430,93 @@ class Context:
                   "fhe_rotate_sum_hoisted")
         return out
 
+    def _rot_keys(self, elts, rot_keys, ct, who):
+        """Host arrays of key pointers (None for the unrotated element 1), shapes checked."""
+        if len(rot_keys) != len(elts):
+            raise ValueError(f"{who}: one key (or None) per Galois element")
+        for g, key in zip(elts, rot_keys):
+            if key is None:
+                if g != 1:
+                    raise ValueError(f"{who}: only Galois element 1 takes no key")
+                continue
+            kb, ka = key
+            if tuple(kb.shape) != (self.dnum, self.L + self.K, self.n) or ka.shape != kb.shape:
+                raise ValueError(f"{who}: keys must be [dnum, L + K, N]")
+            if kb.device != ct.device or ka.device != ct.device or not (
+                    kb.is_contiguous() and ka.is_contiguous()):
+                raise ValueError(f"{who}: keys must be contiguous on the ct's device")
+        k = max(len(elts), 1)
+        return ((ctypes.c_uint32 * k)(*elts),
+                (ctypes.c_void_p * k)(*[kk[0].data_ptr() if kk else None for kk in rot_keys]),
+                (ctypes.c_void_p * k)(*[kk[1].data_ptr() if kk else None for kk in rot_keys]))
+
+    def _pts(self, pts, ct, who):
+        for pt in pts:
+            if tuple(pt.shape) != (self.L + self.K, self.n) or pt.device != ct.device or not \
+                    pt.is_contiguous():
+                raise ValueError(f"{who}: plaintexts must be contiguous [L + K, N] on the ct's "
+                                 "device")
+        return (ctypes.c_void_p * max(len(pts), 1))(*[p.data_ptr() for p in pts])
+
+    def rotate_sum_multi(self, cts, galois_elts, rot_keys, workspace=None, out=None):
+        """sum_r rot_{galois_elts[r]}(cts[r]) over different ciphertexts (each [..., 2, L, N], NTT
+        form, one shape) with one ModDown (fhe_rotate_sum_multi, the giant-step sum of a BSGS
+        linear transform); rot_keys[r] = (rot_b, rot_a) or None for Galois element 1."""
+        if not cts:
+            raise ValueError("rotate_sum_multi: at least one ciphertext")
+        ct = cts[0]
+        _check_tensor(ct, "ct", (2, self.L, self.n))
+        for c in cts:
+            if c.shape != ct.shape or c.device != ct.device or not c.is_contiguous():
+                raise ValueError("rotate_sum_multi: ciphertexts of one shape, contiguous, on one "
+                                 "device")
+        elts = [int(g) for g in galois_elts]
+        if len(cts) != len(elts):
+            raise ValueError("rotate_sum_multi: one Galois element per ciphertext")
+        g_arr, b_arr, a_arr = self._rot_keys(elts, rot_keys, ct, "rotate_sum_multi")
+        batch = ct.numel() // (2 * self.L * self.n)
+        if out is None:
+            out = _empty(*ct.shape, dtype=ct.dtype, device=ct.device)
+        else:
+            _check_out(out, ct, tuple(ct.shape), "rotate_sum_multi: out")
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_rotate_sum_multi_workspace(self._ptr, batch))
+        c_arr = (ctypes.c_void_p * len(cts))(*[c.data_ptr() for c in cts])
+        with torch.cuda.device(self.device):
+            check(lib.fhe_rotate_sum_multi(self._ptr, _ptr(out), c_arr, g_arr, b_arr, a_arr,
+                                           len(elts), batch, _ptr(ws), _stream(ct)),
+                  "fhe_rotate_sum_multi")
+        return out
+
+    def linear_transform(self, ct, baby_elts, baby_keys, giant_elts, giant_keys, pts,
+                         workspace=None, out=None):
+        """Baby-step / giant-step plaintext-matrix product with both hoistings
+        (fhe_linear_transform): sum_g rot_{giant[g]}(sum_b pts[g][b] rot_{baby[b]}(ct)) for
+        ct [..., 2, L, N] NTT form; pts[g][b] [L + K, N] NTT form over Q u P."""
+        _check_tensor(ct, "ct", (2, self.L, self.n))
+        baby = [int(g) for g in baby_elts]
+        giant = [int(g) for g in giant_elts]
+        n1, n2 = len(baby), len(giant)
+        if len(pts) != n2 or any(len(row) != n1 for row in pts):
+            raise ValueError("linear_transform: pts must be n2 lists of n1 plaintexts")
+        bg, bb, ba = self._rot_keys(baby, baby_keys, ct, "linear_transform")
+        gg, gb, ga = self._rot_keys(giant, giant_keys, ct, "linear_transform")
+        p_arr = self._pts([p for row in pts for p in row], ct, "linear_transform")
+        batch = ct.numel() // (2 * self.L * self.n)
+        if out is None:
+            out = _empty(*ct.shape, dtype=ct.dtype, device=ct.device)
+        else:
+            _check_out(out, ct, tuple(ct.shape), "linear_transform: out")
+        lib = load()
+        ws = workspace if workspace is not None else self.workspace(
+            lib.fhe_linear_transform_workspace(self._ptr, n2, batch))
+        with torch.cuda.device(self.device):
+            check(lib.fhe_linear_transform(self._ptr, _ptr(out), _ptr(ct), n1, n2, bg, bb, ba, gg,
+                                           gb, ga, p_arr, batch, _ptr(ws), _stream(ct)),
+                  "fhe_linear_transform")
+        return out
+
     # ---- SURVEY.md §8(f) row 3: sampling, keys, encryption --------------------------------
     # seed=None draws a fresh 64-bit nonce from the OS CSPRNG.  An explicit seed is for
     # reproducible tests: never reuse one per secret key (fhecore.h SECURITY note).

@@ -320,6 +320,35 @@ int fhe_rotate_sum_hoisted(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in
                            const uint64_t* const* rot_a, const uint64_t* const* pt,
                            uint32_t count, uint32_t batch, void* workspace, fhe_stream_t stream);
 
+/* fhe_rotate_sum_multi: out = sum_r rot_{galois_elts[r]}(cts[r]) over `count` (1..16) DIFFERENT
+ * ciphertexts (each [batch][2][L][N] NTT form over Q) with ONE ModDown: per term a ModUp of its own
+ * c1 and its gathered inner product accumulated in Q u P (the giant-step sum of a baby-step /
+ * giant-step linear transform).  galois_elts[r] == 1 adds cts[r] unrotated (no key; rot_b[r] /
+ * rot_a[r] may be null).  out must not overlap any cts[r].  Decrypts to sum_r sigma_r(m_r) up to one
+ * ModDown's rounding.  Restated by oracle/pyoracle.py rotate_sum_multi.  Contexts with dnum <= 8. */
+size_t fhe_rotate_sum_multi_workspace(const fhe_ctx* ctx, uint32_t batch);
+int fhe_rotate_sum_multi(const fhe_ctx* ctx, uint64_t* out, const uint64_t* const* cts,
+                         const uint32_t* galois_elts, const uint64_t* const* rot_b,
+                         const uint64_t* const* rot_a, uint32_t count, uint32_t batch,
+                         void* workspace, fhe_stream_t stream);
+
+/* fhe_linear_transform: the baby-step / giant-step plaintext-matrix product of CKKS bootstrapping
+ * (CoeffToSlot / SlotToCoeff) with both hoistings:
+ *   out = sum_{g < n2} rot_{giant_elts[g]}( sum_{b < n1} pt[g n1 + b] * rot_{baby_elts[b]}(in) ),
+ * n1, n2 in 1..16; pt[g n1 + b] [L + K][N] NTT form over Q u P (the diagonals, pre-rotated by the
+ * caller as BSGS requires); element 1 in either list is an unrotated step (its keys may be null).
+ * ONE ModUp of in's c1 serves every baby step; each giant step's inner sum is exactly
+ * fhe_rotate_sum_hoisted(in, baby_elts, baby keys, pt[g n1 ..]) and the outer sum exactly
+ * fhe_rotate_sum_multi of those.  in, out [batch][2][L][N] NTT form; out must not overlap in.
+ * Restated by oracle/pyoracle.py linear_transform. */
+size_t fhe_linear_transform_workspace(const fhe_ctx* ctx, uint32_t n2, uint32_t batch);
+int fhe_linear_transform(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in, uint32_t n1,
+                         uint32_t n2, const uint32_t* baby_elts, const uint64_t* const* baby_b,
+                         const uint64_t* const* baby_a, const uint32_t* giant_elts,
+                         const uint64_t* const* giant_b, const uint64_t* const* giant_a,
+                         const uint64_t* const* pt, uint32_t batch, void* workspace,
+                         fhe_stream_t stream);
+
 /* ---- wire format (not in the reference) ------------------------------
  * A self-describing little-endian blob for any [polys][nlimbs][N] residue tensor over context
  * limbs [limb0, limb0 + nlimbs) -- ciphertexts, keys, plaintexts: "FHEC", version 1, flags (bit 0

@@ -394,6 +394,34 @@ class Evaluator {
     if (hipStreamSynchronize(s_) != hipSuccess) throw Error(FHE_EDEVICE, "rotate_hoisted: sync");
     return out;
   }
+  // sum_r pts[r] * rot_{galois_elts[r]}(ct) with one ModUp and one ModDown (fhe_rotate_sum_hoisted,
+  // double hoisting: the inner loop of a baby-step / giant-step linear transform).  keys[r] may be
+  // null for galois_elts[r] == 1 (the unrotated term); pts[r] [L + K][N] NTT form over Q u P.
+  Ciphertext rotate_sum(const Ciphertext& ct, const std::vector<uint32_t>& galois_elts,
+                        const std::vector<const SwitchKey*>& keys,
+                        const std::vector<const DeviceBuffer*>& pts) const {
+    if (ct.components != 2 || !ct.ntt_form || ct.limbs != ctx_.L())
+      throw Error(FHE_EINVAL, "rotate_sum: need a 2-component NTT-form ciphertext over L limbs");
+    const size_t count = galois_elts.size();
+    if (keys.size() != count || pts.size() != count)
+      throw Error(FHE_EINVAL, "rotate_sum: one key (or null) and one plaintext per term");
+    std::vector<const uint64_t*> kb(count ? count : 1), ka(count ? count : 1),
+        pp(count ? count : 1);
+    for (size_t r = 0; r < count; ++r) {
+      kb[r] = keys[r] ? keys[r]->b() : nullptr;
+      ka[r] = keys[r] ? keys[r]->a() : nullptr;
+      if (!pts[r] || pts[r]->size() != (size_t)(ctx_.L() + ctx_.K()) * ctx_.n())
+        throw Error(FHE_EINVAL, "rotate_sum: plaintexts are [L + K][N]");
+      pp[r] = pts[r]->data();
+    }
+    Ciphertext out(ctx_, 2, ct.limbs, true);
+    const size_t need = fhe_rotate_sum_hoisted_workspace(ctx_.get(), 1);
+    if (ws_.size() * 8 < need) ws_ = DeviceBuffer((need + 7) / 8);
+    check(fhe_rotate_sum_hoisted(ctx_.get(), out.data(), ct.data(), galois_elts.data(), kb.data(),
+                                 ka.data(), pp.data(), (uint32_t)count, 1, ws_.data(), s_),
+          "fhe_rotate_sum_hoisted");
+    return out;
+  }
 
  private:
   static void same(const Ciphertext& a, const Ciphertext& b, const char* who) {

@@ -663,6 +663,55 @@ def rotate_sum_hoisted(ct_ntt, ks, keys, pts, qs, ps, dnum, log_n: int):
     return np.stack([(s0 + moddown_ntt(a0, qs, ps)) % col, moddown_ntt(a1, qs, ps)])
 
 
+def rotate_sum_multi(cts, ks, keys, qs, ps, dnum, log_n: int):
+    """sum_r rot_{k_r}(cts[r]) over different ciphertexts with ONE ModDown (the giant-step sum of a
+    baby-step / giant-step linear transform), restated for gpu-fhe_amd/csrc/galois.hip
+    launch_rotate_sum_multi.  Per rotated term: ModUp of its own c1, the gathered inner product
+    with its key added into the Q u P sums A_h, sigma_k(c0) into the c0 sum; an unrotated term
+    (k = 1, no key) adds c0 and c1 themselves (exactly: ModDown(P x + y) = x + ModDown(y)).
+      out = (C0 + ModDown(A0), C1 + ModDown(A1)).  (L, N) x 2 out."""
+    qs = [int(q) for q in qs]
+    ps = [int(p) for p in ps]
+    allm = qs + ps
+    L = len(qs)
+    mods = _mods_col(allm)
+    col = _mods_col(qs)
+    n = np.asarray(cts[0]).shape[-1]
+    a0 = np.zeros((len(allm), n), dtype=object)
+    a1 = np.zeros_like(a0)
+    s0 = np.zeros((L, n), dtype=object)
+    s1 = np.zeros_like(s0)
+    for ct, k, key in zip(cts, ks, keys):
+        k = int(k)
+        c0 = np.asarray(ct[0]).astype(object)
+        c1 = np.asarray(ct[1]).astype(object)
+        if k == 1:
+            s0 = (s0 + c0) % col
+            s1 = (s1 + c1) % col
+            continue
+        ext = [rns_ntt_fwd(e, allm) for e in modup(rns_ntt_inv(c1, qs), qs, ps, dnum)]
+        for (lo, hi), e in zip(digit_ranges(L, dnum), ext):
+            e[lo:hi] = c1[lo:hi]
+        rot_b, rot_a = key
+        idx = automorphism_ntt_index(k, log_n)
+        for j, e in enumerate(ext):
+            g = e[..., idx]
+            a0 = (a0 + g * np.asarray(rot_b[j]).astype(object)) % mods
+            a1 = (a1 + g * np.asarray(rot_a[j]).astype(object)) % mods
+        s0 = (s0 + c0[..., idx]) % col
+    return np.stack([(s0 + moddown_ntt(a0, qs, ps)) % col, (s1 + moddown_ntt(a1, qs, ps)) % col])
+
+
+def linear_transform(ct_ntt, baby, baby_keys, giant, giant_keys, pts, qs, ps, dnum, log_n: int):
+    """Baby-step / giant-step plaintext-matrix product with both hoistings, restated for
+    gpu-fhe_amd/csrc/galois.hip launch_linear_transform:
+      out = sum_g rot_{giant[g]}( sum_b pts[g][b] rot_{baby[b]}(ct) ),
+    each giant step's inner sum exactly rotate_sum_hoisted (one ModUp of ct shared by all of them on
+    the device, one ModDown each), the outer sum exactly rotate_sum_multi (one ModDown)."""
+    inner = [rotate_sum_hoisted(ct_ntt, baby, baby_keys, row, qs, ps, dnum, log_n) for row in pts]
+    return rotate_sum_multi(inner, giant, giant_keys, qs, ps, dnum, log_n)
+
+
 def rescale_coeff(x, moduli):
     """Divide-and-round by the last modulus: x (l, N) coefficient form over q_0..q_{l-1} ->
     (l - 1, N) with out_i = floor((X + q_last // 2) / q_last) mod q_i, X the CRT value in

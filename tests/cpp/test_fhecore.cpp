@@ -157,6 +157,25 @@ int main() {
           }
         }
       }
+      // double-hoisted rotation sum with all-ones plaintexts (NTT of the constant 1): decrypts to
+      // sigma_k(m) + sigma_conj(m)
+      {
+        fhe::DeviceBuffer ones((size_t)(kc.L() + kc.K()) * kn);
+        ones.upload(std::vector<u64>((size_t)(kc.L() + kc.K()) * kn, 1));
+        const std::vector<int64_t> rs = decrypt_limb0(kev.rotate_sum(ct, {k, kconj}, {&rk, &ck},
+                                                                     {&ones, &ones}));
+        std::vector<int64_t> want(kn, 0);
+        for (uint32_t g : {k, kconj})
+          for (u64 i = 0; i < kn; ++i) {
+            const u64 t = i * g % (2 * kn);
+            want[t % kn] += t < kn ? m[i] : -m[i];
+          }
+        for (u64 i = 0; i < kn; ++i)
+          if (std::llabs(rs[i] - want[i]) > 2000) {
+            std::printf("FAIL rotation sum coeff %llu\n", (unsigned long long)i);
+            return 1;
+          }
+      }
       const fhe::SwitchKey rl = kg.relin_key(46);
       const fhe::Ciphertext sq = kev.mul_relin(ct, ct, rl, false);
       if (sq.limbs != 3) {

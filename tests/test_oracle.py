@@ -342,6 +342,63 @@ def test_rotation_sum_double_hoisted_decrypts(dnum):
     assert (got.astype(object) == out).all()
 
 
+def _sigma_int(v, k, q):
+    """sigma_k of an integer polynomial (centred mod q)."""
+    r = pyoracle.automorphism_coeff(np.array([[x % q for x in v]], dtype=object), k, [q])[0]
+    return [int(x) - q if int(x) > q // 2 else int(x) for x in r]
+
+
+def test_linear_transform_bsgs_decrypts():
+    """pyoracle.linear_transform (baby-step / giant-step, both hoistings) decrypts to
+    sum_g sigma_{G_g}(sum_b pt_{g,b} sigma_{B_b}(m)) + small noise with unrotated baby and giant
+    steps present; its giant sum (rotate_sum_multi) alone decrypts to sum_r sigma_r(m_r)."""
+    log_n, L, K, dnum = 5, 3, 2, 3
+    n = 1 << log_n
+    mods = pyoracle.gen_moduli(log_n, L + K)
+    qs, ps = mods[:L], mods[L:]
+    allm = qs + ps
+    rng = random.Random(77)
+    s = [rng.randrange(-1, 2) for _ in range(n)]
+    col = pyoracle._mods_col(qs)
+    s_n = pyoracle.rns_ntt_fwd(pyoracle._to_rns(s, qs), qs)
+
+    def enc(m):
+        a = np.stack([np.array([rng.randrange(q) for _ in range(n)], dtype=object) for q in qs])
+        e = pyoracle.rns_ntt_fwd(pyoracle._to_rns([rng.randrange(-3, 4) for _ in range(n)], qs),
+                                 qs)
+        return np.stack([(-a * s_n + e + pyoracle.rns_ntt_fwd(pyoracle._to_rns(m, qs), qs)) % col,
+                         a])
+
+    def dec(ct):
+        return pyoracle.crt_centered(pyoracle.rns_ntt_inv((ct[0] + ct[1] * s_n) % col, qs), qs)
+
+    m = [rng.randrange(-1000, 1000) for _ in range(n)]
+    ct = enc(m)
+    baby = [1, pyoracle.galois_elt(1, n)]
+    giant = [1, pyoracle.galois_elt(2, n), 2 * n - 1]
+    key = lambda k: None if k == 1 else pyoracle.gen_rot_key(s, k, qs, ps, dnum, rng)  # noqa: E731
+    bkeys = [key(k) for k in baby]
+    gkeys = [key(k) for k in giant]
+    pt_int = [[[rng.randrange(-3, 4) for _ in range(n)] for _ in baby] for _ in giant]
+    pts = [[pyoracle.rns_ntt_fwd(pyoracle._to_rns(p, allm), allm) for p in row] for row in pt_int]
+    out = pyoracle.linear_transform(ct, baby, bkeys, giant, gkeys, pts, qs, ps, dnum, log_n)
+    assert out.shape == (2, L, n)
+    want = [0] * n
+    for G, row in zip(giant, pt_int):
+        inner = [0] * n
+        for B, p in zip(baby, row):
+            inner = [w + v for w, v in zip(inner, _negacyclic_int(p, _sigma_int(m, B, qs[0])))]
+        want = [w + v for w, v in zip(want, _sigma_int(inner, G, qs[0]))]
+    assert max(abs(int(d) - w) for d, w in zip(dec(out), want)) < 1 << 24
+    # the giant-step sum on its own: three different ciphertexts
+    ms = [[rng.randrange(-1000, 1000) for _ in range(n)] for _ in giant]
+    outm = pyoracle.rotate_sum_multi([enc(x) for x in ms], giant, gkeys, qs, ps, dnum, log_n)
+    wantm = [0] * n
+    for G, x in zip(giant, ms):
+        wantm = [w + v for w, v in zip(wantm, _sigma_int(x, G, qs[0]))]
+    assert max(abs(int(d) - w) for d, w in zip(dec(outm), wantm)) < 1 << 20
+
+
 # ---- SURVEY.md §8(f) row 3: Philox and samplers ---------------------------------------------
 
 def test_philox_known_answers():
