@@ -439,8 +439,8 @@ int fhe_rotate_sum_hoisted(const fhe_ctx* c, uint64_t* out, const uint64_t* in,
                                    hs(s));
 }
 
-size_t fhe_rotate_sum_multi_workspace(const fhe_ctx* c, uint32_t batch) {
-  return c ? rotate_sum_multi_workspace_bytes(c, batch) : 0;
+size_t fhe_rotate_sum_multi_workspace(const fhe_ctx* c, uint32_t count, uint32_t batch) {
+  return c ? rotate_sum_multi_workspace_bytes(c, count, batch) : 0;
 }
 
 int fhe_rotate_sum_multi(const fhe_ctx* c, uint64_t* out, const uint64_t* const* cts,
@@ -471,7 +471,7 @@ int fhe_rotate_sum_multi(const fhe_ctx* c, uint64_t* out, const uint64_t* const*
       return kInvalid;
     }
   }
-  if ((rc = ensure_ws(c, rotate_sum_multi_workspace_bytes(c, batch), &ws, hs(s)))) return rc;
+  if ((rc = ensure_ws(c, rotate_sum_multi_workspace_bytes(c, count, batch), &ws, hs(s)))) return rc;
   return launch_rotate_sum_multi(c, out, cts, galois_elts, rot_b, rot_a, count, batch, ws, hs(s));
 }
 

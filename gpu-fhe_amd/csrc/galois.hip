@@ -131,14 +131,17 @@ struct RotSumTerms {
   const u64* kb[kRotSumMax];
   const u64* ka[kRotSumMax];
   const u64* pt[kRotSumMax];
+  // per-term ciphertext and ModUp digits (rotate_sum_multi: every term its own); null: the
+  // kernel's in / ext
+  const u64* in[kRotSumMax];
+  const u64* ext[kRotSumMax];
 };
 // 2 ciphertexts per thread: 110 VGPRs, 4 waves per SIMD for the gathers' latency; 4 took 182 (2
 // waves): rot_sum 3.30 -> 2.48 ms per 32 x 8 terms, +18 % terms/s same-box
 // (profiles/r06_rotsum_bc_ab.txt)
 constexpr u32 kRotSumBC = 2;
-// k_rot_sum flags: write the unrotated term's c1 sum (cadd's second half); start from the sums in
-// acc / cadd instead of zero (one launch per term of rotate_sum_multi)
-constexpr int kRotSumC1 = 1, kRotSumAccum = 2;
+// k_rot_sum flags: write the unrotated terms' c1 sum (cadd's second half)
+constexpr int kRotSumC1 = 1;
 
 // a + x y for the rotation sum's 128-bit accumulators: narrow moduli (q < 2^61) add exact
 // products (at most 16 terms of q^2 < 2^122 each); wide ones reduce every product
@@ -173,8 +176,8 @@ __device__ __forceinline__ void rs_mac61(u128& a, u64 x, u64 y) {
 template <int DNUM, bool WIDE, bool FAST = false>
 __global__ __launch_bounds__(kThreads) void k_rot_sum(u64* __restrict__ acc, u64 acc_ws,
                                                       u64* __restrict__ cadd, int flags,
-                                                      const u64* __restrict__ ext,
-                                                      const u64* __restrict__ in,
+                                                      const u64* __restrict__ ext0,
+                                                      const u64* __restrict__ in0,
                                                       const RotSumTerms tm, u32 rows, u32 L,
                                                       u32 alpha, u32 batch, u32 log_n,
                                                       const ModParams* __restrict__ mods) {
@@ -191,23 +194,12 @@ __global__ __launch_bounds__(kThreads) void k_rot_sum(u64* __restrict__ acc, u64
   const u32 b0 = bc * kRotSumBC, nb = min(kRotSumBC, batch - b0);
   u128 s0[kRotSumBC] = {}, s1[kRotSumBC] = {}, a0[kRotSumBC] = {}, a1[kRotSumBC] = {};
   const bool ident = (flags & kRotSumC1) != 0;
-  if (flags & kRotSumAccum) {  // add to the sums a previous launch left (canonical words)
-#pragma unroll
-    for (u32 bb = 0; bb < kRotSumBC; ++bb) {
-      if (bb >= nb) break;
-      const u32 b = b0 + bb;
-      s0[bb] = acc[(u64)b * rn + e];
-      s1[bb] = acc[acc_ws + (u64)b * rn + e];
-      if (r < L) {
-        a0[bb] = cadd[(u64)b * ln + e];
-        if (ident) a1[bb] = cadd[(u64)(batch + b) * ln + e];
-      }
-    }
-  }
   const u32 sh = 32 - log_n, mask2 = (2u << log_n) - 1;
   for (u32 k = 0; k < tm.count; ++k) {
     const u32 g = tm.gal[k];
     const u64 p = tm.pt[k] ? tm.pt[k][e] : 1;  // no plaintext: the term itself (rotate_sum_multi)
+    const u64* __restrict__ in = tm.in[k] ? tm.in[k] : in0;
+    const u64* __restrict__ ext = tm.ext[k] ? tm.ext[k] : ext0;
     if (g == 1) {  // the unrotated term (workgroup-uniform)
       if (r < L) {
 #pragma unroll
@@ -552,9 +544,15 @@ int rotsum_check(const fhe_ctx* c, u32 count, const u32* galois, const char* who
   return kOk;
 }
 
-// ModUp of in's c1 ([batch][2][L][N], NTT form) into the ext region: the prepared INTT (the fused
-// hoisted ModUp's scaled inputs) and the hoisted ModUp (rns.hip, modup_only)
-int rotsum_modup(const fhe_ctx* c, const u64* in, u32 batch, const RotSumWs& w, hipStream_t s) {
+// ModUp of in's c1 ([batch][2][L][N], NTT form) into the ext region at kws (w.kws, or another
+// region of ext_words(c, batch) words: a ModUp-only key-switch writes nothing past its digits):
+// the prepared INTT (the fused hoisted ModUp's scaled inputs) and the hoisted ModUp (rns.hip,
+// modup_only)
+u64 ext_words(const fhe_ctx* c, u32 batch) {
+  return (u64)c->dnum * batch * (c->L + c->K) * c->n;
+}
+int rotsum_modup(const fhe_ctx* c, const u64* in, u32 batch, const RotSumWs& w, hipStream_t s,
+                 u64* kws = nullptr) {
   const u32 L = c->L;
   const u64 ln = (u64)L * c->n;
   const bool prep = ks_prepared(c);
@@ -566,11 +564,11 @@ int rotsum_modup(const fhe_ctx* c, const u64* in, u32 batch, const RotSumWs& w, 
   KsHoist up;
   up.modup_only = true;
   return launch_keyswitch_shard(c, nullptr, nullptr, call, in + ln, nullptr, nullptr, 0, L, batch,
-                                w.kws, s, nullptr, &up);
+                                kws ? kws : w.kws, s, nullptr, &up);
 }
 
 // One k_rot_sum launch over the terms tm of ciphertexts in (whose ModUp is in the ext region when
-// a term is rotated): the accumulators and cadd get the sums (flags: kRotSumC1, kRotSumAccum)
+// a term is rotated): the accumulators and cadd get the sums (flags: kRotSumC1)
 int rotsum_pass(const fhe_ctx* c, const u64* in, const RotSumTerms& tm, int flags, u32 batch,
                 const RotSumWs& w, hipStream_t s) {
   const u32 L = c->L, rows = L + c->K;
@@ -651,39 +649,61 @@ int launch_rotate_sum_hoisted(const fhe_ctx* c, u64* out, const u64* in, const u
   return rotsum_moddown(c, out, in + (u64)c->L * c->n, ident, batch, w, s);
 }
 
-size_t rotate_sum_multi_workspace_bytes(const fhe_ctx* c, u32 batch) {
-  return rotate_sum_hoisted_workspace_bytes(c, batch);
+size_t rotate_sum_multi_workspace_bytes(const fhe_ctx* c, u32 count, u32 batch) {
+  // the rotation sum's workspace, then the ModUp digits of every rotated term past the first
+  return rotate_sum_hoisted_workspace_bytes(c, batch) +
+         (size_t)(count > 1 ? count - 1 : 0) * ext_words(c, batch) * sizeof(u64);
 }
 
+namespace {
+// The giant-step sum: every rotated term's ModUp into its own digit region (the first in w's ext
+// region, the others in `extra`, ext_words each), then ONE k_rot_sum pass over all the terms (each
+// with its own ciphertext and digits, no plaintext: the accumulators are written once) and ONE
+// ModDown.
+int rotsum_multi(const fhe_ctx* c, u64* out, const u64* const* cts, const u32* galois,
+                 const u64* const* rot_b, const u64* const* rot_a, u32 count, u32 batch,
+                 const RotSumWs& w, u64* extra, hipStream_t s) {
+  RotSumTerms tm{};
+  tm.count = count;
+  u32 nrot = 0;
+  for (u32 r = 0; r < count; ++r) {
+    tm.gal[r] = galois[r];
+    tm.kb[r] = rot_b ? rot_b[r] : nullptr;
+    tm.ka[r] = rot_a ? rot_a[r] : nullptr;
+    tm.pt[r] = nullptr;
+    tm.in[r] = cts[r];
+    if (galois[r] == 1) continue;
+    u64* region = nrot == 0 ? w.kws : extra + (u64)(nrot - 1) * ext_words(c, batch);
+    if (int rc = rotsum_modup(c, cts[r], batch, w, s, region)) return rc;
+    tm.ext[r] = region;
+    ++nrot;
+  }
+  int rc;
+  if ((rc = rotsum_pass(c, cts[0], tm, kRotSumC1, batch, w, s))) return rc;
+  return rotsum_moddown(c, out, cts[0] + (u64)c->L * c->n, true, batch, w, s);
+}
+}  // namespace
+
 // sum_r rot_{galois[r]}(cts[r]) over count DIFFERENT ciphertexts with ONE ModDown (the giant-step
-// sum of a baby-step / giant-step linear transform, Bossuat et al.'s second hoisting): per term a
-// ModUp of its own c1 and one accumulating k_rot_sum pass (no plaintext), then one ModDown of the
-// summed accumulators with the sigma(c0) sum (and the unrotated terms' c0, c1) added in its finish.
+// sum of a baby-step / giant-step linear transform, Bossuat et al.'s second hoisting): a ModUp of
+// each rotated term's own c1, one k_rot_sum pass over all the terms, then one ModDown of the summed
+// accumulators with the sigma(c0) sum (and the unrotated terms' c0, c1) added in its finish.
 // Restated by oracle/pyoracle.py rotate_sum_multi.
 int launch_rotate_sum_multi(const fhe_ctx* c, u64* out, const u64* const* cts, const u32* galois,
                             const u64* const* rot_b, const u64* const* rot_a, u32 count,
                             u32 batch, void* ws, hipStream_t s) {
   if (int rc = rotsum_check(c, count, galois, "rotate_sum_multi")) return rc;
   if (batch == 0 || count == 0) return kOk;
-  const RotSumWs w = rotsum_ws(c, ws, batch);
-  for (u32 r = 0; r < count; ++r) {
-    RotSumTerms tm{};
-    tm.count = 1;
-    tm.gal[0] = galois[r];
-    tm.kb[0] = rot_b ? rot_b[r] : nullptr;
-    tm.ka[0] = rot_a ? rot_a[r] : nullptr;
-    tm.pt[0] = nullptr;
-    int rc;
-    if (galois[r] != 1 && (rc = rotsum_modup(c, cts[r], batch, w, s))) return rc;
-    if ((rc = rotsum_pass(c, cts[r], tm, kRotSumC1 | (r > 0 ? kRotSumAccum : 0), batch, w, s)))
-      return rc;
-  }
-  return rotsum_moddown(c, out, cts[0] + (u64)c->L * c->n, true, batch, w, s);
+  u64* extra = reinterpret_cast<u64*>(static_cast<char*>(ws) +
+                                      rotate_sum_hoisted_workspace_bytes(c, batch));
+  return rotsum_multi(c, out, cts, galois, rot_b, rot_a, count, batch, rotsum_ws(c, ws, batch),
+                      extra, s);
 }
 
 size_t linear_transform_workspace_bytes(const fhe_ctx* c, u32 n2, u32 batch) {
-  // the rotation sums' workspace, then the n2 giant-step inputs [n2][batch][2][L][N]
-  return rotate_sum_hoisted_workspace_bytes(c, batch) +
+  // the rotation sums' workspace, the n2 giant-step inputs [n2][batch][2][L][N], then the giant
+  // steps' extra ModUp digit regions (rotate_sum_multi)
+  return rotate_sum_multi_workspace_bytes(c, n2, batch) +
          (size_t)n2 * batch * 2 * c->L * c->n * sizeof(u64);
 }
 
@@ -708,6 +728,7 @@ int launch_linear_transform(const fhe_ctx* c, u64* out, const u64* in, u32 n1, u
   const u64 ct_words = (u64)batch * 2 * c->L * c->n;
   u64* inner = reinterpret_cast<u64*>(static_cast<char*>(ws) +
                                       rotate_sum_hoisted_workspace_bytes(c, batch));
+  u64* extra = inner + (u64)n2 * ct_words;
   bool ident = false, rotated = false;
   for (u32 b = 0; b < n1; ++b) {
     ident = ident || baby[b] == 1;
@@ -731,7 +752,7 @@ int launch_linear_transform(const fhe_ctx* c, u64* out, const u64* in, u32 n1, u
       return rc;
     inner_ptr[g] = ig;
   }
-  return launch_rotate_sum_multi(c, out, inner_ptr, giant, giant_b, giant_a, n2, batch, ws, s);
+  return rotsum_multi(c, out, inner_ptr, giant, giant_b, giant_a, n2, batch, w, extra, s);
 }
 
 }  // namespace fhe

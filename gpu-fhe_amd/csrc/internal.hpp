@@ -391,7 +391,7 @@ size_t rotate_sum_hoisted_workspace_bytes(const fhe_ctx* c, u32 batch);
 int launch_rotate_sum_multi(const fhe_ctx* c, u64* out, const u64* const* cts, const u32* galois,
                             const u64* const* rot_b, const u64* const* rot_a, u32 count,
                             u32 batch, void* ws, hipStream_t s);
-size_t rotate_sum_multi_workspace_bytes(const fhe_ctx* c, u32 batch);
+size_t rotate_sum_multi_workspace_bytes(const fhe_ctx* c, u32 count, u32 batch);
 // out = sum_g rot_{giant[g]}(sum_b pt[g n1 + b] rot_{baby[b]}(in)), both hoistings
 int launch_linear_transform(const fhe_ctx* c, u64* out, const u64* in, u32 n1, u32 n2,
                             const u32* baby, const u64* const* baby_b, const u64* const* baby_a,

@@ -78,7 +78,7 @@ SIGNATURES = {
     "fhe_rotate_hoisted": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     "fhe_rotate_sum_hoisted_workspace": (_sz, [_vp, _u32]),
     "fhe_rotate_sum_hoisted": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
-    "fhe_rotate_sum_multi_workspace": (_sz, [_vp, _u32]),
+    "fhe_rotate_sum_multi_workspace": (_sz, [_vp, _u32, _u32]),
     "fhe_rotate_sum_multi": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     "fhe_linear_transform_workspace": (_sz, [_vp, _u32, _u32]),
     "fhe_linear_transform": (_i32, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

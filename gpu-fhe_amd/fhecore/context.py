@@ -481,7 +481,7 @@ class Context:
             _check_out(out, ct, tuple(ct.shape), "rotate_sum_multi: out")
         lib = load()
         ws = workspace if workspace is not None else self.workspace(
-            lib.fhe_rotate_sum_multi_workspace(self._ptr, batch))
+            lib.fhe_rotate_sum_multi_workspace(self._ptr, len(cts), batch))
         c_arr = (ctypes.c_void_p * len(cts))(*[c.data_ptr() for c in cts])
         with torch.cuda.device(self.device):
             check(lib.fhe_rotate_sum_multi(self._ptr, _ptr(out), c_arr, g_arr, b_arr, a_arr,

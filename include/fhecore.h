@@ -321,12 +321,12 @@ int fhe_rotate_sum_hoisted(const fhe_ctx* ctx, uint64_t* out, const uint64_t* in
                            uint32_t count, uint32_t batch, void* workspace, fhe_stream_t stream);
 
 /* fhe_rotate_sum_multi: out = sum_r rot_{galois_elts[r]}(cts[r]) over `count` (1..16) DIFFERENT
- * ciphertexts (each [batch][2][L][N] NTT form over Q) with ONE ModDown: per term a ModUp of its own
- * c1 and its gathered inner product accumulated in Q u P (the giant-step sum of a baby-step /
- * giant-step linear transform).  galois_elts[r] == 1 adds cts[r] unrotated (no key; rot_b[r] /
+ * ciphertexts (each [batch][2][L][N] NTT form over Q) with ONE ModDown: a ModUp of each rotated
+ * term's own c1 (the workspace holds every term's digits), then one pass forming all the gathered
+ * inner products in Q u P (the giant-step sum of a baby-step / giant-step linear transform).  galois_elts[r] == 1 adds cts[r] unrotated (no key; rot_b[r] /
  * rot_a[r] may be null).  out must not overlap any cts[r].  Decrypts to sum_r sigma_r(m_r) up to one
  * ModDown's rounding.  Restated by oracle/pyoracle.py rotate_sum_multi.  Contexts with dnum <= 8. */
-size_t fhe_rotate_sum_multi_workspace(const fhe_ctx* ctx, uint32_t batch);
+size_t fhe_rotate_sum_multi_workspace(const fhe_ctx* ctx, uint32_t count, uint32_t batch);
 int fhe_rotate_sum_multi(const fhe_ctx* ctx, uint64_t* out, const uint64_t* const* cts,
                          const uint32_t* galois_elts, const uint64_t* const* rot_b,
                          const uint64_t* const* rot_a, uint32_t count, uint32_t batch,

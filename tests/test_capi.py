@@ -77,7 +77,7 @@ def test_errors_are_reported_not_raised():
                                       None) == -1
     assert lib.fhe_rotate_sum_hoisted_workspace(None, 1) == 0
     assert lib.fhe_rotate_sum_multi(None, None, None, None, None, None, 1, 1, None, None) == -1
-    assert lib.fhe_rotate_sum_multi_workspace(None, 1) == 0
+    assert lib.fhe_rotate_sum_multi_workspace(None, 2, 1) == 0
     assert lib.fhe_linear_transform(None, None, None, 1, 1, None, None, None, None, None, None,
                                     None, 1, None, None) == -1
     assert lib.fhe_linear_transform_workspace(None, 1, 1) == 0

@@ -86,6 +86,28 @@ def test_linear_transform_matches_oracle(fc, log_n, L, K, dnum):
         assert (got[b].astype(object) == want).all(), b
 
 
+def test_linear_transform_wide_moduli_match_oracle(fc):
+    """A chain with 62/63-bit moduli (the WIDE k_rot_sum, unfused ModUp / ModDown) and 50-61-bit
+    ones: the transform and its giant-step sum bit-exact vs the oracle."""
+    log_n = 11
+    g = lambda bits, count=1, skip=0: [int(q) for q in fc.gen_moduli(log_n, count, bits=bits,  # noqa: E731
+                                                                     skip=skip)]
+    qs = g(63) + g(60) + g(55) + g(62)
+    ps = g(61) + g(50)
+    ctx = fc.Context(log_n, moduli=qs, special=ps, dnum=2)
+    allm = qs + ps
+    baby = [ctx.galois_elt(1), 1]
+    giant = [1, ctx.galois_elt(-2)]
+    ct = rand(qs, log_n, (2,), seed=17)
+    hb, db = keys_for(fc, baby, allm, log_n, 2, 500)
+    hg, dg = keys_for(fc, giant, allm, log_n, 2, 600)
+    pts = [[rand(allm, log_n, seed=700 + 2 * gg + b) for b in range(2)] for gg in range(2)]
+    got = fc.to_host(ctx.linear_transform(dev(fc, ct), baby, db, giant, dg,
+                                          [[dev(fc, p) for p in row] for row in pts]))
+    want = pyoracle.linear_transform(ct, baby, hb, giant, hg, pts, qs, ps, 2, log_n)
+    assert (got.astype(object) == want).all()
+
+
 def test_linear_transform_decrypts_with_real_keys(fc):
     """Real rotation keys and a real encryption: the transform decrypts to
     sum_g sigma_G(sum_b pt_{g,b} sigma_B(m)) up to noise (and equals the oracle bit for bit)."""
