@@ -12,6 +12,7 @@
  * Spec: SURVEY.md §8a' (forward natural -> bit-reversed, psi^brv twiddles; inverse exact).
  * Nothing in gpu-fhe_amd/ links or calls it. */
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -52,14 +53,20 @@ static int g_nptab = 0;
 static inline u64 shoup_c(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
 
 /* Tables are built serially (prepare) before any parallel region reads them. */
-static const ptab_t* ptab(u64 q, uint32_t log_n) {
+/* Only prepare() builds or recycles entries (fhe_oracle.c get_tables: recycling here could free a
+ * table the same call's prepare() had just built). */
+static const ptab_t* find_ptab(u64 q, uint32_t log_n) {
   for (int i = 0; i < g_nptab; ++i)
     if (g_ptab[i].q == q && g_ptab[i].log_n == log_n) return &g_ptab[i];
+  return NULL;
+}
+
+static const ptab_t* ptab(u64 q, uint32_t log_n) {
+  const ptab_t* found = find_ptab(q, log_n);
+  if (found) return found;
   if (g_nptab == MAX_PTAB) {
-    for (int i = 0; i < g_nptab; ++i) {
-      free(g_ptab[i].w); free(g_ptab[i].ws); free(g_ptab[i].wi); free(g_ptab[i].wis);
-    }
-    g_nptab = 0;
+    fprintf(stderr, "fhe_cpu_port: table cache full outside prepare()\n");
+    abort();
   }
   ptab_t* t = &g_ptab[g_nptab++];
   const u64 n = 1ull << log_n;
@@ -159,6 +166,14 @@ static inline u64 redc(u128 t, u64 q, u64 qi) {
 }
 
 static void prepare(uint32_t log_n, const u64* moduli, uint32_t L) {
+  uint32_t missing = 0;
+  for (uint32_t l = 0; l < L; ++l) missing += find_ptab(moduli[l], log_n) == NULL;
+  if (g_nptab + missing > MAX_PTAB) { /* recycle everything before building this call's tables */
+    for (int i = 0; i < g_nptab; ++i) {
+      free(g_ptab[i].w); free(g_ptab[i].ws); free(g_ptab[i].wi); free(g_ptab[i].wis);
+    }
+    g_nptab = 0;
+  }
   for (uint32_t l = 0; l < L; ++l) ptab(moduli[l], log_n);
 }
 

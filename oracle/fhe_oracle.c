@@ -15,6 +15,7 @@
  * Threading: OpenMP over (poly, limb) pairs.
  */
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -149,14 +150,23 @@ typedef struct {
 static tables_t g_tab[MAX_TABLES];
 static int g_ntab = 0;
 
-static const tables_t* get_tables(u64 q, uint32_t log_n) {
+/* The table cache.  Only prepare() (serial, before any parallel region of its caller) may build
+ * or recycle entries; the parallel regions only look them up.  (Recycling inside get_tables, as
+ * this file first did, could free a table an earlier prepare() of the same call had just built
+ * once ~256 distinct moduli had passed through one process, and the parallel lookups then built
+ * entries concurrently: wrong expected values in a long test session.) */
+static const tables_t* find_tables(u64 q, uint32_t log_n) {
   for (int i = 0; i < g_ntab; ++i)
     if (g_tab[i].q == q && g_tab[i].log_n == log_n) return &g_tab[i];
-  if (g_ntab == MAX_TABLES) { /* recycle */
-    for (int i = 0; i < g_ntab; ++i) {
-      free(g_tab[i].w); free(g_tab[i].ws); free(g_tab[i].wi); free(g_tab[i].wis);
-    }
-    g_ntab = 0;
+  return NULL;
+}
+
+static const tables_t* get_tables(u64 q, uint32_t log_n) {
+  const tables_t* found = find_tables(q, log_n);
+  if (found) return found;
+  if (g_ntab == MAX_TABLES) {
+    fprintf(stderr, "fhe_oracle: table cache full outside prepare()\n");
+    abort();
   }
   tables_t* t = &g_tab[g_ntab++];
   u64 n = 1ull << log_n;
@@ -233,6 +243,14 @@ static void ntt_inv_1(u64* a, const tables_t* t) {
 }
 
 static void prepare(uint32_t log_n, const u64* moduli, uint32_t L) {
+  uint32_t missing = 0;
+  for (uint32_t l = 0; l < L; ++l) missing += find_tables(moduli[l], log_n) == NULL;
+  if (g_ntab + missing > MAX_TABLES) { /* recycle everything before building this call's tables */
+    for (int i = 0; i < g_ntab; ++i) {
+      free(g_tab[i].w); free(g_tab[i].ws); free(g_tab[i].wi); free(g_tab[i].wis);
+    }
+    g_ntab = 0;
+  }
   for (uint32_t l = 0; l < L; ++l) get_tables(moduli[l], log_n);
 }
 

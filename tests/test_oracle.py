@@ -468,3 +468,22 @@ def test_cpu_port_keyswitch_matches_oracle(log_n, L, K, dnum):
     for b in range(B):
         r0, r1 = coracle.keyswitch(d2[b], eb, ea, qs, ps, dnum)
         assert (k0[b] == r0).all() and (k1[b] == r1).all()
+
+
+def test_c_table_cache_survives_recycling():
+    """More distinct (q, log N) pairs than the C oracle's table cache holds (256) in one process:
+    every call still transforms with its own moduli's tables.  (The cache once recycled inside a
+    lookup, freeing tables the same call had just built, so that its OpenMP workers rebuilt entries
+    concurrently: wrong expected values late in a long GPU test session.)"""
+    log_n = 6
+    mods = [int(q) for q in coracle.gen_moduli(log_n, 300, bits=40)]
+    rng = np.random.default_rng(9)
+    for start in range(0, 300 - 8, 7):  # overlapping windows of 8: the cache fills mid-call
+        qs = mods[start:start + 8]
+        x = np.stack([rng.integers(0, q, size=(1 << log_n,), dtype=np.uint64) for q in qs])
+        got = coracle.ntt_fwd(x, qs)
+        if start % 35 == 0:
+            want = np.stack([np.array(pyoracle.ntt_fwd(list(map(int, x[i])), q), dtype=np.uint64)
+                             for i, q in enumerate(qs)])
+            assert (got == want).all(), start
+        assert (coracle.ntt_inv(got, qs) == x).all(), start
